@@ -1,0 +1,196 @@
+"""Throughput bench of the MI355X CWT engine (driver contract: one JSON line).
+
+Default workload (the north_star target, BASELINE.json configs[3]): Morse CWT of
+512 epochs x 64 channels x 16384 samples x 256 freqs PER GPU, fp32 -- weak
+scaling, so 8 GPUs process the full 4096-epoch config.  A "step" is one pass of
+the hot path over that batch: forward rocFFT of every signal, then the
+spectrum-multiply / inverse-FFT engine writing every (signal, freq, sample)
+output point to HBM.  Inputs are resident in HBM before timing starts; the
+complex output (1.1 TB per GPU per step) is streamed through two rotating HBM
+chunk buffers.  Signals are sharded over ranks with no collective on the data
+path (the barrier and a max-reduce of the elapsed time are timing only).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config c4|c3|c2] [--engine auto|rocfft|fused]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBPS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
+
+CONFIGS = {
+    # name: (kind, epochs per GPU, chans, n, freqs, out, dtype, workload text)
+    'c4': ('morse', 512, 64, 16384, np.arange(1, 257, dtype=np.float64), 'cwt', 'float32',
+           'C4 Morse CWT, 512 epochs x 64 ch x 16384 samples x 256 freqs per GPU '
+           '(4096 epochs at 8 GPUs), complex64 out'),
+    'c3': ('morse', 512, 64, 4096, np.arange(1, 257, dtype=np.float64), 'power', 'float32',
+           'C3 Morse power, 512 epochs x 64 ch x 4096 samples x 256 freqs per GPU, float32 out'),
+    'c2': ('morlet', 1, 64, 16384, np.arange(1, 129, dtype=np.float64), 'cwt', 'float32',
+           'C2 Morlet CWT, 64 ch x 16384 samples x 128 freqs per GPU, complex64 out'),
+}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def synth_device(torch, S, n, seed, device, sfreq=1000.):
+    """Synthetic multi-channel sinusoids + noise, generated on the device."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x = torch.empty((S, n), dtype=torch.float32, device=device)
+    t = torch.arange(n, device=device, dtype=torch.float64) / sfreq
+    step = 1024
+    for s0 in range(0, S, step):
+        s1 = min(S, s0 + step)
+        fc = torch.rand((s1 - s0, 1), generator=g, device=device, dtype=torch.float64) * 99 + 1
+        ph = torch.rand((s1 - s0, 1), generator=g, device=device, dtype=torch.float64) * 2 * np.pi
+        noise = torch.randn((s1 - s0, n), generator=g, device=device, dtype=torch.float32)
+        x[s0:s1] = (torch.sin(2 * np.pi * fc * t + ph)).float() + 0.1 * noise
+    return x
+
+
+def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0):
+    """The CPU oracle (numpy + scipy.fftpack, the reference's arithmetic) on one core,
+    W built once (reuse=True) and excluded, timed over as many signals as fit the budget."""
+    from oracle import nw_oracle as O
+    rng = np.random.default_rng(0)
+    t = np.arange(n) / 1000.
+    rows = O.fft_wavelets(kind, freqs, 1000., n / 1000., False)
+    done, t0 = 0, time.perf_counter()
+    while True:
+        x = np.sin(2 * np.pi * rng.uniform(1, 100) * t) + 0.1 * rng.standard_normal(n)
+        y = O.cwt_from_rows(x, rows, False)
+        if out_kind == 'power':
+            y = np.abs(y) ** 2
+        done += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s and done >= 3:
+            break
+    pts = done * len(freqs) * n
+    return {'value': pts / el, 'unit': 'points/s', 'cores': 1, 'kind': 'port',
+            'sample': f'{done} signals x {len(freqs)} freqs x {n} samples ({kind} {out_kind}, '
+                      f'oracle/nw_oracle.py single process, wavelet table cached), {el:.1f} s'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', default='c4', choices=sorted(CONFIGS))
+    ap.add_argument('--engine', default='auto', choices=['auto', 'rocfft', 'fused'])
+    ap.add_argument('--chunk', type=int, default=256, help='signals per device chunk')
+    ap.add_argument('--epochs', type=int, default=None, help='override epochs per GPU')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import ninwavelets_amd as nw
+    from ninwavelets_amd import _lib as L
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+    torch.cuda.set_device(dev)
+
+    kind, epochs, chans, n, freqs, out_kind, dtype, text = CONFIGS[args.config]
+    if args.epochs:
+        epochs = args.epochs
+    S = epochs * chans                       # signals on this rank
+    F = len(freqs)
+    C = min(args.chunk, S)
+    x = synth_device(torch, S, n, seed=1000 + rank, device=dev)
+    odt = torch.complex64 if out_kind == 'cwt' else torch.float32
+    bufs = [torch.empty((C, F, n), dtype=odt, device=dev) for _ in range(2)]
+    plan = nw.Plan(n, F, dtype, device=local, max_batch=C,
+                   engine=None if args.engine == 'auto' else args.engine, timing=True)
+    grid = L.trans_grid(n / 1000., 1000., False)
+    params = {'morse': [17.5, 3.0], 'morlet': [7.0, 0.0]}[kind]
+    plan.set_wavelet(kind, params, freqs, grid)
+    esz = 4
+    x_ptr, x_row = x.data_ptr(), n * esz
+
+    def step():
+        for i, s0 in enumerate(range(0, S, C)):
+            c = min(C, S - s0)
+            plan.execute_ptr(x_ptr + s0 * x_row, c, bufs[i & 1].data_ptr(), out_kind)
+
+    def barrier():
+        torch.cuda.synchronize()
+        plan.sync()
+        if world > 1:
+            dist.barrier()
+
+    log(f'[bench] rank {rank}/{world} {args.config}: S={S} n={n} F={F} chunk={C} '
+        f'engine={plan.stats()["engine"]}')
+    for w in range(args.warmup):
+        step()
+        barrier()
+        log(f'[bench] warmup {w + 1}/{args.warmup} done')
+    plan.reset_stats()
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    st = plan.stats()
+    points = float(S) * F * n * args.steps * world
+    value = points / el
+
+    if rank == 0:
+        # dominant kernel: the fused kernel, or K1 (the spectrum multiply) on the rocFFT engine
+        fused = st['engine'] == 'fused'
+        launches = st['launches_fused'] if fused else st['launches_multiply']
+        ms = (st['ms_fused'] if fused else st['ms_multiply']) / max(1, launches)
+        out_e = (2 if out_kind == 'cwt' else 1) * esz
+        if not fused:
+            out_e = 2 * esz                    # K1 always writes the complex product
+        per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
+        achieved = per_launch / (ms * 1e-3) / 1e9
+        roof = {'kernel': 'nw_fused' if fused else 'k1_multiply', 'bound': 'hbm',
+                'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
+                'frac': round(achieved / PEAK_HBM_GBPS, 4), 'traffic': None,
+                'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
+        stage_ms = {k: round(st[k] / args.steps, 3) for k in
+                    ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_copy')}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            log('[bench] cpu baseline ...')
+            cpu = cpu_baseline(kind, n, freqs, out_kind)
+        line = {
+            'metric': 'CWT throughput (epochs*chans*samples*freqs)/s',
+            'value': value, 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'config': {'workload': text, 'wavelet': kind, 'epochs': epochs * world, 'chans': chans,
+                       'samples': n, 'freqs': F, 'output': out_kind, 'engine': st['engine'],
+                       'chunk_signals': C, 'parallelism': f'dp{world} (signals sharded, no collective)'},
+            'roofline': roof, 'cpu_baseline': cpu, 'stage_ms_per_step': stage_ms,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

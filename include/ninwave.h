@@ -1,0 +1,145 @@
+/*
+ * ninwave.h — C ABI of libninwave.so, the MI355X (gfx950) FFT-domain CWT engine.
+ *
+ * This is the drop-in boundary for ninwavelets' hot path:
+ *   WaveletBase.cwt / power / abs         reference base.py:378-443
+ *   WaveletBase.make_fft_wavelet(s)       reference base.py:221-279
+ *   WaveletBase._setup_trans_shape        reference base.py:173-194
+ *   pad_to / interpolate_alias            reference base.py:75-82, 107-123
+ *   Morse / Morlet / Shannon spectra      reference wavelets.py:65-74, 132-136, 256-262
+ *   EpochsWavelet.cwt (batched caller)    reference mneutils.py:26-40
+ * The reference is pure Python/numpy, so it has no FFI of its own; the Python
+ * host layer (ninwavelets_amd/_lib.py, ctypes) binds exactly these symbols, and
+ * INTEGRATION.md shows the binding a maintainer would add to the reference.
+ *
+ * Conventions
+ *  - Every function returns int status: NW_OK (0) or a negative NW_E* code;
+ *    nw_last_error() returns a thread-local message for the last failure.
+ *  - Plain pointers and sizes only.  Host buffers are C-contiguous row-major.
+ *  - A plan is bound to one device and one HIP stream; it is not reentrant.
+ *  - Complex numbers are interleaved (re, im) of the plan's real dtype.
+ */
+#ifndef NINWAVE_H
+#define NINWAVE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define NW_OK              0
+#define NW_E_INVALID      -1   /* bad argument (maps to ValueError) */
+#define NW_E_HIP          -2   /* HIP runtime error */
+#define NW_E_ROCFFT       -3   /* rocFFT error */
+#define NW_E_NOMEM        -4   /* device allocation failed */
+#define NW_E_STATE        -5   /* call out of order (e.g. execute before set_wavelet) */
+#define NW_E_NODEVICE     -6   /* no HIP device visible */
+
+/* compute dtypes (the arithmetic type of the whole path) */
+#define NW_F32 0
+#define NW_F64 1
+
+/* wavelet kinds */
+#define NW_MORSE   1   /* params: b, r                      wavelets.py:38-74  */
+#define NW_MORLET  2   /* params: sigma, gabor(0/1)         wavelets.py:110-144 */
+#define NW_SHANNON 3   /* params: none (freq is ignored)    wavelets.py:256-262 */
+#define NW_TABLE   4   /* complex128 rows supplied by the host (WaveletMode.Normal,
+                          user plugins overriding trans_formula/formula)          */
+
+/* plan flags */
+#define NW_INTERPOLATE   0x1u  /* zero the upper half of fft(x) (interpolate_alias, base.py:400-401) */
+#define NW_ENGINE_ROCFFT 0x10u /* force: rocFFT fwd -> K1 multiply -> rocFFT inv -> K2 epilogue   */
+#define NW_ENGINE_FUSED  0x20u /* force: rocFFT fwd -> fused multiply+LDS inverse FFT+epilogue     */
+#define NW_TIMING        0x100u/* record HIP events around every stage (nw_plan_stats)            */
+
+/* execute outputs */
+#define NW_OUT_CWT   0   /* complex (S, F, N)   base.py:378-407 */
+#define NW_OUT_ABS   1   /* real    (S, F, N)   base.py:427-443 */
+#define NW_OUT_POWER 2   /* real    (S, F, N)   base.py:409-425 */
+
+/* memory placement of x / out in nw_execute */
+#define NW_MEM_HOST   0
+#define NW_MEM_DEVICE 1
+
+/* Analytic-spectrum grid of one cache build (base.py:173-194, 238-246, 274-276):
+ *   nu_j = j * delta for j < len_valid, and zero for len_valid <= j < len_full.
+ * delta = 1/(n/sfreq); len_full is the row length of the reference's cached
+ * wavelet (len(np.arange(...)), doubled by the hstack when interpolating). */
+typedef struct nw_grid {
+    double  delta;
+    int64_t len_full;
+    int64_t len_valid;
+} nw_grid;
+
+/* Per-stage device time accumulated since the plan was created or reset. */
+typedef struct nw_stats {
+    int64_t executes;       /* nw_execute calls */
+    int64_t chunks;         /* device chunks run */
+    double  ms_forward;     /* rocFFT forward (R2C) */
+    double  ms_multiply;    /* K1 spectrum multiply (rocFFT engine) */
+    double  ms_inverse;     /* rocFFT inverse (rocFFT engine) */
+    double  ms_epilogue;    /* K2 |.| / |.|^2 (rocFFT engine) */
+    double  ms_fused;       /* fused multiply + inverse FFT + epilogue (fused engine) */
+    double  ms_copy;        /* host<->device copies */
+    int64_t launches_multiply;
+    int64_t launches_fused;
+    int64_t engine;         /* NW_ENGINE_ROCFFT or NW_ENGINE_FUSED actually used */
+} nw_stats;
+
+typedef struct nw_plan nw_plan;
+
+const char* nw_last_error(void);
+const char* nw_version(void);
+int nw_device_count(int* n);
+
+/* Host-only (no GPU): the grid of the reference's make_fft_wavelet(freq, real_length)
+ * -- cwt passes real_length = n / sfreq (base.py:395).  Replaces _setup_trans_shape
+ * (base.py:173-194) as called from base.py:238-245. */
+int nw_trans_grid(double real_length, double sfreq, int interpolate, nw_grid* grid);
+
+/* Host-only (no GPU): whether the fused engine supports (n, dtype). */
+int nw_fused_supported(int64_t n, int dtype);
+
+/* Create a plan for signals of n samples, up to max_batch signals per device
+ * chunk, nfreq scales.  flags: NW_INTERPOLATE | NW_ENGINE_* | NW_TIMING. */
+int nw_plan_create(nw_plan** plan, int device, int64_t n, int64_t max_batch,
+                   int32_t nfreq, int dtype, uint32_t flags);
+
+/* Attach the wavelet (the reference's cached fft_wavelets, base.py:258-279).
+ *   freqs[nfreq]: scale frequencies; grid: the cache-build grid (nw_trans_grid of
+ *   the build length -- it may differ from the plan's n: base.py:394-397 reuses
+ *   the cache and pad_to's it to the current n).
+ *   params: NW_MORSE {b, r}; NW_MORLET {sigma, gabor[, c, k]} (c, k of wavelets.py:118-122,
+ *   derived from sigma when absent); NW_SHANNON {}; NW_TABLE {}.
+ *   table: NW_TABLE only, complex128 [nfreq][grid.len_full], copied to the device. */
+int nw_plan_set_wavelet(nw_plan* plan, int kind, const double* params, int nparams,
+                        const double* freqs, const nw_grid* grid, const void* table);
+
+/* Evaluate the attached wavelet rows on the device and copy them to the host:
+ * out[nfreq][grid.len_full] of the plan dtype (real for analytic kinds, complex
+ * for NW_TABLE) -- the reference's self.fft_wavelets. */
+int nw_plan_wavelet_rows(nw_plan* plan, void* out_host);
+
+/* Run the CWT of nsig signals x[nsig][n] (plan dtype) into out[nsig][nfreq][n]
+ * (complex for NW_OUT_CWT, real otherwise).  mem = NW_MEM_HOST: synchronous;
+ * NW_MEM_DEVICE: x/out are device pointers on the plan's device, the call is
+ * asynchronous on the plan stream (see nw_plan_sync). */
+int nw_execute(nw_plan* plan, const void* x, int64_t nsig, void* out, int out_kind, int mem);
+
+/* Shard nsig host signals over ndev plans (one per device, identical config),
+ * one host thread per device; contiguous blocks of signals per device. */
+int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t nsig,
+                     void* out, int out_kind);
+
+int nw_plan_set_stream(nw_plan* plan, void* hip_stream);   /* NULL: the plan's own stream */
+int nw_plan_sync(nw_plan* plan);
+int nw_plan_stats(nw_plan* plan, nw_stats* stats);
+int nw_plan_reset_stats(nw_plan* plan);
+int nw_plan_destroy(nw_plan* plan);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NINWAVE_H */

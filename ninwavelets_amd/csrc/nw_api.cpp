@@ -1,0 +1,597 @@
+// nw_api.cpp — the C ABI of libninwave.so (include/ninwave.h).
+//
+// Pipeline per device chunk of signals:
+//   x (S, n) --H2D/D2D--> d_x --rocFFT R2C--> d_X (S, n/2+1)
+//   engine ROCFFT: K1 multiply -> d_Y (S, F, n) -> rocFFT C2C inverse in place -> K2 epilogue
+//   engine FUSED : one kernel: W*X -> LDS Stockham inverse FFT -> epilogue store
+// The wavelet is never materialised on the host: analytic kinds are evaluated
+// inside the kernels from (kind, params, freqs, grid).
+#include <hip/hip_runtime.h>
+#include <rocfft/rocfft.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "nw_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+    g_last_error = msg;
+    return code;
+}
+
+#define NW_HIP(expr)                                                                          \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(e_ == hipErrorOutOfMemory ? NW_E_NOMEM : NW_E_HIP,                    \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                   \
+    } while (0)
+
+#define NW_RF(expr)                                                                           \
+    do {                                                                                      \
+        rocfft_status s_ = (expr);                                                            \
+        if (s_ != rocfft_status_success)                                                      \
+            return fail(NW_E_ROCFFT, std::string(#expr) + ": rocfft status " + std::to_string((int)s_)); \
+    } while (0)
+
+#define NW_TRY(expr)                 \
+    do {                             \
+        int r_ = (expr);             \
+        if (r_ != NW_OK) return r_;  \
+    } while (0)
+
+std::once_flag g_rocfft_once;
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+enum Stage { ST_FWD = 0, ST_MUL, ST_INV, ST_EPI, ST_FUSED, ST_COPY, ST_N };
+
+struct Pending {
+    int stage;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct nw_plan {
+    int device = 0;
+    int64_t n = 0, nh = 0, max_batch = 0;
+    int nfreq = 0, dtype = NW_F32;
+    uint32_t flags = 0;
+    int engine = NW_ENGINE_ROCFFT;
+    size_t esz = 4;  // real element size
+
+    hipStream_t own_stream = nullptr, stream = nullptr;
+
+    // wavelet
+    bool has_wavelet = false;
+    nw::WDesc desc{};
+    double* d_freq = nullptr;
+    double* d_peak = nullptr;
+    float* d_xstep32 = nullptr;
+    void* d_table = nullptr;
+
+    // buffers
+    void* d_x = nullptr;
+    void* d_X = nullptr;
+    void* d_Y = nullptr;
+    size_t d_Y_bytes = 0;
+    void* d_out = nullptr;
+    size_t d_out_bytes = 0;
+
+    // rocFFT, keyed by batch count
+    std::map<int64_t, rocfft_plan> fwd, inv;
+    rocfft_execution_info info = nullptr;
+    void* work = nullptr;
+    size_t work_bytes = 0;
+
+    // timing
+    std::vector<Pending> pending;
+    std::vector<hipEvent_t> event_pool;
+    nw_stats stats{};
+};
+
+namespace {
+
+int ensure(void** ptr, size_t* cur, size_t want) {
+    if (*cur >= want && *ptr) return NW_OK;
+    if (*ptr) {
+        NW_HIP(hipFree(*ptr));
+        *ptr = nullptr;
+        *cur = 0;
+    }
+    NW_HIP(hipMalloc(ptr, want));
+    *cur = want;
+    return NW_OK;
+}
+
+int take_event(nw_plan* p, hipEvent_t* ev) {
+    if (!p->event_pool.empty()) {
+        *ev = p->event_pool.back();
+        p->event_pool.pop_back();
+        return NW_OK;
+    }
+    NW_HIP(hipEventCreate(ev));
+    return NW_OK;
+}
+
+// Run `fn` on the plan stream, bracketed by events when NW_TIMING is set.
+template <typename F>
+int staged(nw_plan* p, int stage, F&& fn) {
+    if (!(p->flags & NW_TIMING)) return fn();
+    Pending pe{stage, nullptr, nullptr};
+    NW_TRY(take_event(p, &pe.a));
+    NW_TRY(take_event(p, &pe.b));
+    NW_HIP(hipEventRecord(pe.a, p->stream));
+    int r = fn();
+    NW_HIP(hipEventRecord(pe.b, p->stream));
+    p->pending.push_back(pe);
+    return r;
+}
+
+int resolve_timing(nw_plan* p) {
+    if (p->pending.empty()) return NW_OK;
+    NW_HIP(hipStreamSynchronize(p->stream));
+    for (const Pending& pe : p->pending) {
+        float ms = 0.f;
+        NW_HIP(hipEventElapsedTime(&ms, pe.a, pe.b));
+        switch (pe.stage) {
+            case ST_FWD: p->stats.ms_forward += ms; break;
+            case ST_MUL: p->stats.ms_multiply += ms; p->stats.launches_multiply++; break;
+            case ST_INV: p->stats.ms_inverse += ms; break;
+            case ST_EPI: p->stats.ms_epilogue += ms; break;
+            case ST_FUSED: p->stats.ms_fused += ms; p->stats.launches_fused++; break;
+            default: p->stats.ms_copy += ms; break;
+        }
+        p->event_pool.push_back(pe.a);
+        p->event_pool.push_back(pe.b);
+    }
+    p->pending.clear();
+    return NW_OK;
+}
+
+rocfft_precision prec(const nw_plan* p) {
+    return p->dtype == NW_F32 ? rocfft_precision_single : rocfft_precision_double;
+}
+
+int get_rocfft_plans(nw_plan* p, int64_t batch, rocfft_plan* fwd, rocfft_plan* inv) {
+    auto itf = p->fwd.find(batch);
+    if (itf == p->fwd.end()) {
+        size_t len = (size_t)p->n;
+        rocfft_plan pf = nullptr;
+        NW_RF(rocfft_plan_create(&pf, rocfft_placement_notinplace, rocfft_transform_type_real_forward, prec(p), 1,
+                                 &len, (size_t)batch, nullptr));
+        p->fwd[batch] = pf;
+        size_t ws = 0;
+        NW_RF(rocfft_plan_get_work_buffer_size(pf, &ws));
+        if (ws > p->work_bytes) NW_TRY(ensure(&p->work, &p->work_bytes, ws));
+        itf = p->fwd.find(batch);
+    }
+    *fwd = itf->second;
+    if (inv) {
+        auto iti = p->inv.find(batch);
+        if (iti == p->inv.end()) {
+            size_t len = (size_t)p->n;
+            rocfft_plan pi = nullptr;
+            NW_RF(rocfft_plan_create(&pi, rocfft_placement_inplace, rocfft_transform_type_complex_inverse, prec(p), 1,
+                                     &len, (size_t)(batch * p->nfreq), nullptr));
+            p->inv[batch] = pi;
+            size_t ws = 0;
+            NW_RF(rocfft_plan_get_work_buffer_size(pi, &ws));
+            if (ws > p->work_bytes) NW_TRY(ensure(&p->work, &p->work_bytes, ws));
+            iti = p->inv.find(batch);
+        }
+        *inv = iti->second;
+    }
+    return NW_OK;
+}
+
+int run_fft(nw_plan* p, rocfft_plan plan, void* in, void* out) {
+    NW_RF(rocfft_execution_info_set_stream(p->info, p->stream));
+    if (p->work_bytes) NW_RF(rocfft_execution_info_set_work_buffer(p->info, p->work, p->work_bytes));
+    void* ib[1] = {in};
+    void* ob[1] = {out};
+    NW_RF(rocfft_execute(plan, ib, out ? ob : nullptr, p->info));
+    return NW_OK;
+}
+
+// One device chunk: xs (device, c signals) -> dst (device).
+int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
+    rocfft_plan fwd = nullptr, inv = nullptr;
+    const bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
+    NW_TRY(get_rocfft_plans(p, c, &fwd, rocfft_engine ? &inv : nullptr));
+    // rocFFT may use its input as scratch: transform from the plan's own copy.
+    if (xs_dev != p->d_x)
+        NW_TRY(staged(p, ST_COPY, [&] {
+            NW_HIP(hipMemcpyAsync(p->d_x, xs_dev, (size_t)c * p->n * p->esz, hipMemcpyDeviceToDevice, p->stream));
+            return NW_OK;
+        }));
+    NW_TRY(staged(p, ST_FWD, [&] { return run_fft(p, fwd, p->d_x, p->d_X); }));
+
+    if (!rocfft_engine) {
+        return staged(p, ST_FUSED, [&] {
+            NW_HIP(nw::launch_fused(p->desc, p->dtype, out_kind, p->d_X, dst, c, p->stream));
+            return NW_OK;
+        });
+    }
+    // K1 writes the product straight into the destination when the caller wants
+    // the complex CWT on the device; otherwise into the plan's Y buffer.
+    void* Y = (out_kind == NW_OUT_CWT && dst_is_final) ? dst : p->d_Y;
+    NW_TRY(staged(p, ST_MUL, [&] {
+        NW_HIP(nw::launch_multiply(p->desc, p->dtype, p->d_X, Y, c, p->stream));
+        return NW_OK;
+    }));
+    NW_TRY(staged(p, ST_INV, [&] { return run_fft(p, inv, Y, nullptr); }));
+    if (out_kind == NW_OUT_CWT) {
+        if (Y != dst)
+            NW_TRY(staged(p, ST_COPY, [&] {
+                NW_HIP(hipMemcpyAsync(dst, Y, (size_t)c * p->nfreq * p->n * 2 * p->esz, hipMemcpyDeviceToDevice,
+                                      p->stream));
+                return NW_OK;
+            }));
+        return NW_OK;
+    }
+    return staged(p, ST_EPI, [&] {
+        NW_HIP(nw::launch_epilogue(p->dtype, out_kind, Y, dst, c * p->nfreq * p->n, p->stream));
+        return NW_OK;
+    });
+}
+
+void free_plan(nw_plan* p) {
+    for (auto& kv : p->fwd) rocfft_plan_destroy(kv.second);
+    for (auto& kv : p->inv) rocfft_plan_destroy(kv.second);
+    if (p->info) rocfft_execution_info_destroy(p->info);
+    void* bufs[] = {p->work, p->d_x, p->d_X, p->d_Y, p->d_out, p->d_freq, p->d_peak, p->d_xstep32, p->d_table};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    for (auto& pe : p->pending) {
+        (void)hipEventDestroy(pe.a);
+        (void)hipEventDestroy(pe.b);
+    }
+    for (auto e : p->event_pool) (void)hipEventDestroy(e);
+    if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
+    delete p;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* nw_last_error(void) { return g_last_error.c_str(); }
+
+const char* nw_version(void) { return "ninwave 0.1.0 (gfx950)"; }
+
+int nw_device_count(int* n) {
+    if (!n) return fail(NW_E_INVALID, "nw_device_count: null pointer");
+    int c = 0;
+    hipError_t e = hipGetDeviceCount(&c);
+    if (e != hipSuccess) {
+        *n = 0;
+        return fail(NW_E_NODEVICE, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    }
+    *n = c;
+    return NW_OK;
+}
+
+// np.arange(0, total, one) length: ceil((stop - start) / step), as numpy's
+// _calc_length does for Python-float arguments (start = 0).
+static int64_t arange_len(double stop, double step) {
+    const double q = stop / step;
+    if (q == 0.0 && stop != 0.0) return std::signbit(q) ? 0 : 1;
+    if (!(q > 0.0)) return 0;
+    return (int64_t)std::ceil(q);
+}
+
+int nw_trans_grid(double real_length, double sfreq, int interpolate, nw_grid* g) {
+    if (!g || !(real_length > 0.0) || !(sfreq > 0.0))
+        return fail(NW_E_INVALID, "nw_trans_grid: need real_length > 0, sfreq > 0");
+    // make_fft_wavelet(freq, real_length) -> _setup_trans_shape(real_length, rl'):
+    //   one = 1 / real_length; total = sfreq / real_length * rl'   (base.py:191-194, 238-245)
+    const double rl = real_length;
+    const double one = 1.0 / rl;
+    const double rwl = interpolate ? rl / 2.0 : rl;
+    const double total = sfreq / rl * rwl;
+    const int64_t len = arange_len(total, one);
+    g->delta = one;
+    g->len_valid = len;
+    g->len_full = interpolate ? 2 * len : len;   // hstack with zeros(len(t)) (base.py:241-242)
+    return NW_OK;
+}
+
+int nw_fused_supported(int64_t n, int dtype) { return nw::fused_supported(n, dtype) ? 1 : 0; }
+
+int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int32_t nfreq, int dtype,
+                   uint32_t flags) {
+    if (!out) return fail(NW_E_INVALID, "nw_plan_create: null plan pointer");
+    *out = nullptr;
+    if (n < 1 || max_batch < 1 || nfreq < 1) return fail(NW_E_INVALID, "nw_plan_create: n, max_batch, nfreq must be >= 1");
+    if (dtype != NW_F32 && dtype != NW_F64) return fail(NW_E_INVALID, "nw_plan_create: dtype must be NW_F32 or NW_F64");
+    if ((flags & NW_ENGINE_ROCFFT) && (flags & NW_ENGINE_FUSED))
+        return fail(NW_E_INVALID, "nw_plan_create: choose one engine");
+    int ndev = 0;
+    NW_TRY(nw_device_count(&ndev));
+    if (ndev == 0) return fail(NW_E_NODEVICE, "nw_plan_create: no HIP device");
+    if (device < 0 || device >= ndev) return fail(NW_E_INVALID, "nw_plan_create: device out of range");
+    std::call_once(g_rocfft_once, [] { rocfft_setup(); });
+
+    DeviceGuard guard(device);
+    nw_plan* p = new nw_plan();
+    p->device = device;
+    p->n = n;
+    p->nh = n / 2 + 1;
+    p->max_batch = max_batch;
+    p->nfreq = nfreq;
+    p->dtype = dtype;
+    p->flags = flags;
+    p->esz = dtype == NW_F32 ? 4 : 8;
+    const bool fused_ok = nw::fused_supported(n, dtype);
+    if (flags & NW_ENGINE_FUSED) {
+        if (!fused_ok) {
+            free_plan(p);
+            return fail(NW_E_INVALID, "nw_plan_create: fused engine does not support this n/dtype");
+        }
+        p->engine = NW_ENGINE_FUSED;
+    } else if (flags & NW_ENGINE_ROCFFT) {
+        p->engine = NW_ENGINE_ROCFFT;
+    } else {
+        p->engine = fused_ok ? NW_ENGINE_FUSED : NW_ENGINE_ROCFFT;
+    }
+    p->stats.engine = p->engine;
+    auto bail = [&](int code) {
+        free_plan(p);
+        return code;
+    };
+    hipError_t e = hipStreamCreateWithFlags(&p->own_stream, hipStreamNonBlocking);
+    if (e != hipSuccess) return bail(fail(NW_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e)));
+    p->stream = p->own_stream;
+    if (rocfft_execution_info_create(&p->info) != rocfft_status_success)
+        return bail(fail(NW_E_ROCFFT, "rocfft_execution_info_create failed"));
+    size_t sz = 0;
+    int r = ensure(&p->d_x, &sz, (size_t)max_batch * n * p->esz);
+    if (r != NW_OK) return bail(r);
+    sz = 0;
+    r = ensure(&p->d_X, &sz, (size_t)max_batch * p->nh * 2 * p->esz);
+    if (r != NW_OK) return bail(r);
+    if (p->engine == NW_ENGINE_ROCFFT) {
+        r = ensure(&p->d_Y, &p->d_Y_bytes, (size_t)max_batch * nfreq * n * 2 * p->esz);
+        if (r != NW_OK) return bail(r);
+    }
+    if (p->engine == NW_ENGINE_FUSED) {
+        e = nw::fused_prepare(n, dtype);
+        if (e != hipSuccess) return bail(fail(NW_E_HIP, std::string("fused_prepare: ") + hipGetErrorString(e)));
+    }
+    *out = p;
+    return NW_OK;
+}
+
+int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams, const double* freqs,
+                        const nw_grid* grid, const void* table) {
+    if (!p || !freqs || !grid) return fail(NW_E_INVALID, "nw_plan_set_wavelet: null argument");
+    if (kind < NW_MORSE || kind > NW_TABLE) return fail(NW_E_INVALID, "nw_plan_set_wavelet: unknown kind");
+    if (kind == NW_TABLE && !table) return fail(NW_E_INVALID, "nw_plan_set_wavelet: NW_TABLE needs a table");
+    if (grid->len_full < 0 || grid->len_valid < 0 || grid->len_valid > grid->len_full)
+        return fail(NW_E_INVALID, "nw_plan_set_wavelet: bad grid lengths");
+    const int F = p->nfreq;
+    for (int i = 0; i < F; ++i)
+        if (kind != NW_TABLE && kind != NW_SHANNON && freqs[i] == 0.0)
+            return fail(NW_E_INVALID, "nw_plan_set_wavelet: freq == 0 (ZeroDivisionError in base.py:234-235)");
+    DeviceGuard guard(p->device);
+    nw::WDesc d{};
+    d.kind = kind;
+    d.nfreq = F;
+    d.delta = grid->delta;
+    d.len_full = grid->len_full;
+    d.len_valid = grid->len_valid;
+    std::vector<double> peak(F, 1.0);
+    std::vector<float> xstep(F, 0.f);
+    if (kind == NW_MORSE) {
+        d.b = nparams > 0 ? params[0] : 17.5;
+        d.r = nparams > 1 ? params[1] : 3.0;
+        d.b_over_r = d.b / d.r;
+        for (int i = 0; i < F; ++i) xstep[i] = (float)(grid->delta / freqs[i]);
+    } else if (kind == NW_MORLET) {
+        d.sigma = nparams > 0 ? params[0] : 7.0;
+        const bool gabor = nparams > 1 && params[1] != 0.0;
+        const double s2 = d.sigma * d.sigma;
+        const double c = std::pow(1.0 + std::exp(-s2) - 2.0 * std::exp(-3.0 / 4.0 * s2), -0.5);
+        d.cpi = (nparams > 2 ? params[2] : c) * std::pow(M_PI, -0.25);
+        d.kappa = nparams > 3 ? params[3] : (gabor ? 0.0 : std::exp(-std::pow(d.sigma, 2.0) / 2.0));
+        for (int i = 0; i < F; ++i) {
+            peak[i] = d.sigma / (1.0 - std::exp(-d.sigma * freqs[i]));
+            xstep[i] = (float)(grid->delta / freqs[i] * peak[i]);
+        }
+    }
+    size_t cur = 0;
+    if (!p->d_freq) {
+        NW_TRY(ensure((void**)&p->d_freq, &cur, F * sizeof(double)));
+        cur = 0;
+        NW_TRY(ensure((void**)&p->d_peak, &cur, F * sizeof(double)));
+        cur = 0;
+        NW_TRY(ensure((void**)&p->d_xstep32, &cur, F * sizeof(float)));
+    }
+    NW_HIP(hipMemcpy(p->d_freq, freqs, F * sizeof(double), hipMemcpyHostToDevice));
+    NW_HIP(hipMemcpy(p->d_peak, peak.data(), F * sizeof(double), hipMemcpyHostToDevice));
+    NW_HIP(hipMemcpy(p->d_xstep32, xstep.data(), F * sizeof(float), hipMemcpyHostToDevice));
+    if (p->d_table) {
+        NW_HIP(hipFree(p->d_table));
+        p->d_table = nullptr;
+    }
+    if (kind == NW_TABLE && grid->len_full > 0) {
+        const size_t cnt = (size_t)F * grid->len_full;
+        const size_t bytes = cnt * 2 * p->esz;
+        NW_HIP(hipMalloc(&p->d_table, bytes));
+        if (p->dtype == NW_F64) {
+            NW_HIP(hipMemcpy(p->d_table, table, bytes, hipMemcpyHostToDevice));
+        } else {
+            std::vector<float> tmp(cnt * 2);
+            const double* src = (const double*)table;
+            for (size_t i = 0; i < cnt * 2; ++i) tmp[i] = (float)src[i];
+            NW_HIP(hipMemcpy(p->d_table, tmp.data(), bytes, hipMemcpyHostToDevice));
+        }
+    }
+    d.freq = p->d_freq;
+    d.peak = p->d_peak;
+    d.xstep32 = p->d_xstep32;
+    d.table = p->d_table;
+    p->desc = d;
+    p->has_wavelet = true;
+    return NW_OK;
+}
+
+int nw_plan_wavelet_rows(nw_plan* p, void* out_host) {
+    if (!p || !out_host) return fail(NW_E_INVALID, "nw_plan_wavelet_rows: null argument");
+    if (!p->has_wavelet) return fail(NW_E_STATE, "nw_plan_wavelet_rows: no wavelet attached");
+    if (p->desc.len_full == 0) return NW_OK;
+    DeviceGuard guard(p->device);
+    const size_t bytes = (size_t)p->nfreq * p->desc.len_full * p->esz * (p->desc.kind == NW_TABLE ? 2 : 1);
+    void* d_rows = nullptr;
+    NW_HIP(hipMalloc(&d_rows, bytes));
+    hipError_t e = nw::launch_rows(p->desc, p->dtype, d_rows, p->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(out_host, d_rows, bytes, hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    (void)hipFree(d_rows);
+    if (e != hipSuccess) return fail(NW_E_HIP, std::string("nw_plan_wavelet_rows: ") + hipGetErrorString(e));
+    return NW_OK;
+}
+
+int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind, int mem) {
+    if (!p || (!x && nsig > 0) || (!out && nsig > 0)) return fail(NW_E_INVALID, "nw_execute: null argument");
+    if (!p->has_wavelet) return fail(NW_E_STATE, "nw_execute: nw_plan_set_wavelet first");
+    if (out_kind < NW_OUT_CWT || out_kind > NW_OUT_POWER) return fail(NW_E_INVALID, "nw_execute: bad out_kind");
+    if (mem != NW_MEM_HOST && mem != NW_MEM_DEVICE) return fail(NW_E_INVALID, "nw_execute: bad mem");
+    if (nsig < 0) return fail(NW_E_INVALID, "nw_execute: nsig < 0");
+    if (nsig == 0) return NW_OK;
+    DeviceGuard guard(p->device);
+    // execute-time geometry: pad_to the cached rows to n, mask X (base.py:396-401)
+    nw::WDesc& d = p->desc;
+    d.n = p->n;
+    d.nh = p->nh;
+    d.scale = 1.0 / (double)p->n;
+    d.off = d.len_full < p->n ? (p->n - d.len_full) / 2 : 0;
+    d.xlim = (p->flags & NW_INTERPOLATE) ? p->n / 2 : p->n;   // int(n / 2) (base.py:120)
+
+    const size_t out_elem = (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
+    const size_t row_out = (size_t)p->nfreq * p->n * out_elem;  // one signal's output bytes
+    const bool host = mem == NW_MEM_HOST;
+    if (host && out_kind != NW_OUT_CWT && p->engine == NW_ENGINE_ROCFFT)
+        NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * row_out));
+    if (host && p->engine == NW_ENGINE_FUSED) NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * row_out));
+    // (rocFFT engine, host CWT: the complex result is read back straight from d_Y)
+
+    for (int64_t s0 = 0; s0 < nsig; s0 += p->max_batch) {
+        const int64_t c = std::min<int64_t>(p->max_batch, nsig - s0);
+        const char* xs = (const char*)x + (size_t)s0 * p->n * p->esz;
+        char* os = (char*)out + (size_t)s0 * row_out;
+        if (host) {
+            NW_TRY(staged(p, ST_COPY, [&] {
+                NW_HIP(hipMemcpyAsync(p->d_x, xs, (size_t)c * p->n * p->esz, hipMemcpyHostToDevice, p->stream));
+                return NW_OK;
+            }));
+            void* dst = (p->engine == NW_ENGINE_ROCFFT && out_kind == NW_OUT_CWT) ? p->d_Y : p->d_out;
+            NW_TRY(run_chunk(p, p->d_x, c, dst, out_kind, true));
+            NW_TRY(staged(p, ST_COPY, [&] {
+                NW_HIP(hipMemcpyAsync(os, dst, (size_t)c * row_out, hipMemcpyDeviceToHost, p->stream));
+                return NW_OK;
+            }));
+            NW_HIP(hipStreamSynchronize(p->stream));
+        } else {
+            NW_TRY(run_chunk(p, xs, c, os, out_kind, true));
+        }
+        p->stats.chunks++;
+    }
+    p->stats.executes++;
+    if (host) NW_TRY(resolve_timing(p));
+    return NW_OK;
+}
+
+int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t nsig, void* out, int out_kind) {
+    if (!plans || nplans < 1) return fail(NW_E_INVALID, "nw_execute_multi: no plans");
+    for (int i = 1; i < nplans; ++i)
+        if (!plans[i] || plans[i]->n != plans[0]->n || plans[i]->nfreq != plans[0]->nfreq ||
+            plans[i]->dtype != plans[0]->dtype)
+            return fail(NW_E_INVALID, "nw_execute_multi: plans must share n, nfreq and dtype");
+    const nw_plan* p0 = plans[0];
+    const size_t x_row = (size_t)p0->n * p0->esz;
+    const size_t o_row = (size_t)p0->nfreq * p0->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p0->esz;
+    const int64_t per = (nsig + nplans - 1) / nplans;
+    std::vector<int> rc(nplans, NW_OK);
+    std::vector<std::string> err(nplans);
+    std::vector<std::thread> th;
+    for (int i = 0; i < nplans; ++i) {
+        const int64_t s0 = std::min<int64_t>(nsig, (int64_t)i * per);
+        const int64_t cnt = std::min<int64_t>(nsig, s0 + per) - s0;
+        if (cnt <= 0) continue;
+        th.emplace_back([&, i, s0, cnt] {
+            rc[i] = nw_execute(plans[i], (const char*)x + s0 * x_row, cnt, (char*)out + s0 * o_row, out_kind,
+                               NW_MEM_HOST);
+            if (rc[i] != NW_OK) err[i] = g_last_error;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int i = 0; i < nplans; ++i)
+        if (rc[i] != NW_OK)
+            return fail(rc[i], "device " + std::to_string(plans[i]->device) + ": " + err[i]);
+    return NW_OK;
+}
+
+int nw_plan_set_stream(nw_plan* p, void* stream) {
+    if (!p) return fail(NW_E_INVALID, "nw_plan_set_stream: null plan");
+    p->stream = stream ? (hipStream_t)stream : p->own_stream;
+    return NW_OK;
+}
+
+int nw_plan_sync(nw_plan* p) {
+    if (!p) return fail(NW_E_INVALID, "nw_plan_sync: null plan");
+    DeviceGuard guard(p->device);
+    NW_HIP(hipStreamSynchronize(p->stream));
+    return resolve_timing(p);
+}
+
+int nw_plan_stats(nw_plan* p, nw_stats* s) {
+    if (!p || !s) return fail(NW_E_INVALID, "nw_plan_stats: null argument");
+    DeviceGuard guard(p->device);
+    NW_TRY(resolve_timing(p));
+    *s = p->stats;
+    return NW_OK;
+}
+
+int nw_plan_reset_stats(nw_plan* p) {
+    if (!p) return fail(NW_E_INVALID, "nw_plan_reset_stats: null plan");
+    DeviceGuard guard(p->device);
+    NW_TRY(resolve_timing(p));
+    const int64_t engine = p->stats.engine;
+    p->stats = nw_stats{};
+    p->stats.engine = engine;
+    return NW_OK;
+}
+
+int nw_plan_destroy(nw_plan* p) {
+    if (!p) return NW_OK;
+    DeviceGuard guard(p->device);
+    (void)hipStreamSynchronize(p->stream);
+    free_plan(p);
+    return NW_OK;
+}
+
+}  // extern "C"

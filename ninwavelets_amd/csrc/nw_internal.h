@@ -1,0 +1,129 @@
+// nw_internal.h — types shared by the C ABI (nw_api.cpp) and the gfx950 kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ninwave.h"
+
+namespace nw {
+
+// Everything a kernel needs to evaluate W[f, k] and to mask X, for one execute.
+//
+// The wavelet row of the reference's cache (base.py:258-279) has len_full bins,
+// bin j carrying psi_f(j * delta) for j < len_valid (analytic kinds) or the
+// host-supplied table value.  At execute time cwt() pad_to's it to the signal
+// length n (base.py:75-82, 396-397): crop when len_full > n, else centre-pad by
+// off = (n - len_full) // 2.  So output bin k uses row bin j = k - off, valid
+// iff 0 <= j < len_valid.  X bins k >= xlim are zeroed (interpolate_alias on
+// fft(x), base.py:400-401).  scale = 1/n folds scipy's ifft normalisation.
+struct WDesc {
+    int     kind;
+    int     nfreq;
+    int64_t n;          // signal length at execute
+    int64_t nh;         // n/2 + 1: row length of the R2C half spectrum
+    int64_t off;
+    int64_t len_valid;
+    int64_t len_full;
+    int64_t xlim;
+    double  delta;      // grid spacing of the cache build
+    double  scale;      // 1/n
+    // Morse (wavelets.py:65-74)
+    double  b, r, b_over_r;
+    // Morlet (wavelets.py:118-136): cpi = c * pi^(-1/4), kappa = k
+    double  sigma, cpi, kappa;
+    // per-frequency device arrays [nfreq]
+    const double* freq;      // f
+    const double* peak;      // Morlet p(f) = sigma / (1 - exp(-sigma f))
+    const float*  xstep32;   // fp32 path: (float)(delta / f)  (Morse) or (float)(delta / f * p(f)) (Morlet)
+    const void*   table;     // NW_TABLE: complex[nfreq][len_full] of the plan dtype
+};
+
+template <typename T> struct cplx { T re, im; };
+
+// ---------------------------------------------------------------------------
+// Analytic spectra.  fp64 follows the reference expression order exactly;
+// fp32 evaluates Morse in the log2 domain (x^b overflows fp32).
+// ---------------------------------------------------------------------------
+
+__device__ __forceinline__ double psi_f64(const WDesc& d, int fi, int64_t j) {
+    const double nu = (double)j * d.delta;               // np.arange fill: j * step
+    if (d.kind == NW_MORSE) {
+        const double x = nu / d.freq[fi];
+        const double step = x > 0.0 ? 1.0 : (x == 0.0 ? x : 0.0);   // np.heaviside(x, x)
+        return 2.0 * (step * pow(x, d.b) * exp(d.b_over_r * (1.0 - pow(x, d.r))));
+    } else if (d.kind == NW_MORLET) {
+        const double x = nu / d.freq[fi] * d.peak[fi];
+        const double a = d.sigma - x;
+        return d.cpi * (exp(-(a * a) / 2.0) - d.kappa * exp(-(x * x) / 2.0));
+    } else {  // NW_SHANNON: 1 for nu <= 1, freq unused
+        return nu <= 1.0 ? 1.0 : 0.0;
+    }
+}
+
+__device__ __forceinline__ float psi_f32(const WDesc& d, int fi, int64_t j) {
+    if (d.kind == NW_MORSE) {
+        const float x = (float)j * d.xstep32[fi];
+        if (!(x > 0.0f)) return 0.0f;
+        const float lx = __log2f(x);
+        // log2(psi/2) = b*log2(x) + (b/r)*log2(e)*(1 - x^r)
+        const float e2 = (float)d.b * lx
+                       + (float)(d.b_over_r * 1.4426950408889634) * (1.0f - exp2f((float)d.r * lx));
+        return 2.0f * exp2f(e2);
+    } else if (d.kind == NW_MORLET) {
+        const float x = (float)j * d.xstep32[fi];
+        const float a = (float)d.sigma - x;
+        return (float)d.cpi * (expf(-(a * a) * 0.5f) - (float)d.kappa * expf(-(x * x) * 0.5f));
+    } else {
+        const double nu = (double)j * d.delta;
+        return nu <= 1.0 ? 1.0f : 0.0f;
+    }
+}
+
+template <typename T> __device__ __forceinline__ T psi(const WDesc& d, int fi, int64_t j);
+template <> __device__ __forceinline__ double psi<double>(const WDesc& d, int fi, int64_t j) { return psi_f64(d, fi, j); }
+template <> __device__ __forceinline__ float  psi<float >(const WDesc& d, int fi, int64_t j) { return psi_f32(d, fi, j); }
+
+// W[f, k] for output bin k (scaled by 1/n), complex in general (TABLE rows).
+template <typename T>
+__device__ __forceinline__ cplx<T> wavelet_bin(const WDesc& d, int fi, int64_t k) {
+    const int64_t j = k - d.off;
+    cplx<T> w{T(0), T(0)};
+    if (j >= 0 && j < d.len_valid) {
+        if (d.kind == NW_TABLE) {
+            const cplx<T> t = reinterpret_cast<const cplx<T>*>(d.table)[(int64_t)fi * d.len_full + j];
+            w.re = t.re * (T)d.scale;
+            w.im = t.im * (T)d.scale;
+        } else {
+            w.re = psi<T>(d, fi, j) * (T)d.scale;
+        }
+    }
+    return w;
+}
+
+// X[k] of a real signal from its R2C half spectrum (conjugate symmetry), masked.
+template <typename T>
+__device__ __forceinline__ cplx<T> spectrum_bin(const cplx<T>* __restrict__ Xs, const WDesc& d, int64_t k) {
+    cplx<T> x{T(0), T(0)};
+    if (k < d.xlim) {
+        if (k < d.nh) {
+            x = Xs[k];
+        } else {
+            x = Xs[d.n - k];
+            x.im = -x.im;
+        }
+    }
+    return x;
+}
+
+// launchers (nw_kernels.hip)
+hipError_t launch_multiply(const WDesc& d, int dtype, const void* X, void* Y, int64_t nsig, hipStream_t s);
+hipError_t launch_epilogue(int dtype, int out_kind, const void* Y, void* out, int64_t count, hipStream_t s);
+hipError_t launch_rows(const WDesc& d, int dtype, void* rows, hipStream_t s);
+// fused engine (nw_fused.hip)
+bool       fused_supported(int64_t n, int dtype);
+hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, void* out,
+                        int64_t nsig, hipStream_t s);
+hipError_t fused_prepare(int64_t n, int dtype);
+
+}  // namespace nw

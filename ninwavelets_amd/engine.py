@@ -1,0 +1,175 @@
+"""Thin Python owner of one ``nw_plan`` (one device, one signal length n).
+
+This is the batched entry point that replaces the serial per-epoch loop of
+the reference (mneutils.py:39): one call transforms S = epochs x channels
+signals.  Inputs/outputs may be numpy arrays (host, synchronous) or device
+buffers (torch tensors on the plan's device or raw pointers; asynchronous on
+the plan stream).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib as L
+
+OUT_KINDS = {'cwt': L.NW_OUT_CWT, 'abs': L.NW_OUT_ABS, 'power': L.NW_OUT_POWER}
+KINDS = {'morse': L.NW_MORSE, 'morlet': L.NW_MORLET, 'shannon': L.NW_SHANNON, 'table': L.NW_TABLE}
+
+
+def np_dtype(dtype) -> np.dtype:
+    dt = np.dtype(dtype)
+    if dt not in (np.float32, np.float64):
+        raise ValueError(f'compute dtype must be float32 or float64, got {dt}')
+    return dt
+
+
+def out_dtype(dtype, out_kind: str) -> np.dtype:
+    dt = np_dtype(dtype)
+    if out_kind == 'cwt':
+        return np.dtype(np.complex64 if dt == np.float32 else np.complex128)
+    return dt
+
+
+def _is_device_tensor(a) -> bool:
+    return hasattr(a, 'data_ptr') and getattr(a, 'is_cuda', False)
+
+
+class Plan:
+    """One nw_plan: signals of length ``n``, ``nfreq`` scales, compute ``dtype``."""
+
+    def __init__(self, n: int, nfreq: int, dtype='float32', device: int = 0, max_batch: int = 1,
+                 interpolate: bool = False, engine: str | None = None, timing: bool = False):
+        self.n, self.nfreq, self.device, self.max_batch = int(n), int(nfreq), int(device), int(max_batch)
+        self.dtype = np_dtype(dtype)
+        self.interpolate = bool(interpolate)
+        flags = L.NW_INTERPOLATE if interpolate else 0
+        if engine == 'rocfft':
+            flags |= L.NW_ENGINE_ROCFFT
+        elif engine == 'fused':
+            flags |= L.NW_ENGINE_FUSED
+        elif engine not in (None, 'auto'):
+            raise ValueError(f'engine must be rocfft, fused or auto, got {engine!r}')
+        if timing:
+            flags |= L.NW_TIMING
+        self._h = ctypes.c_void_p()
+        L.check(L.lib().nw_plan_create(ctypes.byref(self._h), self.device, self.n, self.max_batch,
+                                       self.nfreq, L.NW_F32 if self.dtype == np.float32 else L.NW_F64,
+                                       flags))
+        self.wavelet_token = None
+
+    # -- wavelet -----------------------------------------------------------------
+    def set_wavelet(self, kind: str, params, freqs, grid: L.nw_grid, table=None, token=None):
+        freqs = np.ascontiguousarray(freqs, dtype=np.float64)
+        if freqs.shape != (self.nfreq,):
+            raise ValueError(f'expected {self.nfreq} freqs, got {freqs.shape}')
+        p = np.ascontiguousarray(params if params is not None else [], dtype=np.float64)
+        tab_ptr = None
+        if KINDS[kind] == L.NW_TABLE:
+            table = np.ascontiguousarray(table, dtype=np.complex128)
+            if table.shape != (self.nfreq, grid.len_full):
+                raise ValueError(f'table must be ({self.nfreq}, {grid.len_full}), got {table.shape}')
+            tab_ptr = table.ctypes.data_as(ctypes.c_void_p)
+        L.check(L.lib().nw_plan_set_wavelet(
+            self._h, KINDS[kind], p.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(p.size),
+            freqs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(grid), tab_ptr))
+        self.kind, self.grid = kind, grid
+        self.wavelet_token = token
+
+    def rows(self) -> np.ndarray:
+        """Device-evaluated cached wavelet rows (nfreq, len_full)."""
+        dt = self.dtype if self.kind != 'table' else out_dtype(self.dtype, 'cwt')
+        out = np.empty((self.nfreq, self.grid.len_full), dtype=dt)
+        L.check(L.lib().nw_plan_wavelet_rows(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out
+
+    # -- execute -----------------------------------------------------------------
+    def execute(self, x, out=None, out_kind: str = 'cwt'):
+        """x: (S, n) numpy array (host) -> returns (S, nfreq, n); or device tensors."""
+        kind = OUT_KINDS[out_kind]
+        if _is_device_tensor(x):
+            if out is None:
+                raise ValueError('device execute needs an output tensor')
+            nsig = x.numel() // self.n
+            self._check_device_buffers(x, out, nsig, out_kind)
+            L.check(L.lib().nw_execute(self._h, ctypes.c_void_p(x.data_ptr()), nsig,
+                                       ctypes.c_void_p(out.data_ptr()), kind, L.NW_MEM_DEVICE))
+            return out
+        x = np.ascontiguousarray(x, dtype=self.dtype)
+        if x.shape[-1] != self.n:
+            raise ValueError(f'signal length {x.shape[-1]} != plan n {self.n}')
+        lead = x.shape[:-1]
+        nsig = int(np.prod(lead)) if lead else 1
+        odt = out_dtype(self.dtype, out_kind)
+        if out is None:
+            out = np.empty(lead + (self.nfreq, self.n), dtype=odt)
+        elif out.dtype != odt or not out.flags.c_contiguous or out.size != nsig * self.nfreq * self.n:
+            raise ValueError('out must be a C-contiguous array of the right dtype and size')
+        L.check(L.lib().nw_execute(self._h, x.ctypes.data_as(ctypes.c_void_p), nsig,
+                                   out.ctypes.data_as(ctypes.c_void_p), kind, L.NW_MEM_HOST))
+        return out
+
+    def execute_ptr(self, x_ptr: int, nsig: int, out_ptr: int, out_kind: str = 'cwt'):
+        """Raw device pointers on the plan's device (asynchronous on the plan stream)."""
+        L.check(L.lib().nw_execute(self._h, ctypes.c_void_p(x_ptr), int(nsig), ctypes.c_void_p(out_ptr),
+                                   OUT_KINDS[out_kind], L.NW_MEM_DEVICE))
+
+    def _check_device_buffers(self, x, out, nsig, out_kind):
+        import torch
+        want_x = torch.float32 if self.dtype == np.float32 else torch.float64
+        want_o = {('cwt', np.float32): torch.complex64, ('cwt', np.float64): torch.complex128}.get(
+            (out_kind, self.dtype.type), want_x)
+        if x.dtype != want_x or out.dtype != want_o:
+            raise ValueError(f'device buffers must be {want_x} in / {want_o} out')
+        if not (x.is_contiguous() and out.is_contiguous()):
+            raise ValueError('device buffers must be contiguous')
+        if x.numel() != nsig * self.n or out.numel() != nsig * self.nfreq * self.n:
+            raise ValueError('device buffer sizes do not match (S, n) -> (S, nfreq, n)')
+        if x.device.index != self.device or out.device.index != self.device:
+            raise ValueError(f'device buffers must live on device {self.device}')
+
+    # -- misc --------------------------------------------------------------------
+    def set_stream(self, stream_ptr: int | None):
+        L.check(L.lib().nw_plan_set_stream(self._h, ctypes.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def sync(self):
+        L.check(L.lib().nw_plan_sync(self._h))
+
+    def stats(self) -> dict:
+        s = L.nw_stats()
+        L.check(L.lib().nw_plan_stats(self._h, ctypes.byref(s)))
+        d = s.as_dict()
+        d['engine'] = 'fused' if d['engine'] == L.NW_ENGINE_FUSED else 'rocfft'
+        return d
+
+    def reset_stats(self):
+        L.check(L.lib().nw_plan_reset_stats(self._h))
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if getattr(self, '_h', None) and self._h.value:
+            L.lib().nw_plan_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def execute_multi(plans, x: np.ndarray, out_kind: str = 'cwt') -> np.ndarray:
+    """Shard host signals over several single-device plans (one host thread each)."""
+    p0 = plans[0]
+    x = np.ascontiguousarray(x, dtype=p0.dtype)
+    lead = x.shape[:-1]
+    nsig = int(np.prod(lead)) if lead else 1
+    out = np.empty(lead + (p0.nfreq, p0.n), dtype=out_dtype(p0.dtype, out_kind))
+    arr = (ctypes.c_void_p * len(plans))(*[p.handle.value for p in plans])
+    L.check(L.lib().nw_execute_multi(arr, len(plans), x.ctypes.data_as(ctypes.c_void_p), nsig,
+                                     out.ctypes.data_as(ctypes.c_void_p), OUT_KINDS[out_kind]))
+    return out

@@ -1,0 +1,36 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (runs on the GPU box via gpurun)')
+
+
+def golden_names(prefix=''):
+    return sorted(f[:-4] for f in os.listdir(GOLDEN)
+                  if f.endswith('.npz') and f.startswith(prefix))
+
+
+def load_golden(name):
+    with np.load(os.path.join(GOLDEN, name + '.npz'), allow_pickle=False) as z:
+        d = {k: z[k] for k in z.files}
+    d['meta'] = json.loads(str(d['meta']))
+    return d
+
+
+@pytest.fixture(scope='session')
+def gpu_available():
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False

@@ -1,0 +1,210 @@
+"""GPU parity: the HIP path (through the C ABI) against the reference's own outputs
+(golden vectors made by tests/golden/make_golden.py) and against the CPU oracle.
+
+Tolerances (north_star: "within a stated fp64/fp32 tolerance"):
+  fp64 compute:  max|out - ref| <= 1e-12 * max|ref|
+  fp32 compute:  max|out - ref| <= 1e-5  * max|ref|   (2e-5 for |.|^2 outputs)
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+from oracle import nw_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import ninwavelets_amd as nw  # noqa: E402
+
+TOL = {'float64': 1e-12, 'float32': 1e-5}
+ENGINES = ['rocfft', 'auto']
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs'))]
+CLASSES = {'morse': nw.Morse, 'morlet': nw.Morlet, 'shannon': nw.Shannon,
+           'mexican_hat': nw.MexicanHat, 'haar': nw.Haar}
+
+
+def make(kind, sfreq, interpolate, params, dtype, engine):
+    p = dict(params)
+    return CLASSES[kind](sfreq, interpolate=interpolate, dtype=dtype, engine=engine, **p)
+
+
+def rel_err(got, ref):
+    scale = max(np.max(np.abs(ref)), 1e-300)
+    return np.max(np.abs(got - ref)) / scale
+
+
+def tol(dtype, op):
+    return TOL[dtype] * (2 if op == 'power' else 1)
+
+
+@pytest.mark.parametrize('engine', ENGINES)
+@pytest.mark.parametrize('dtype', ['float64', 'float32'])
+@pytest.mark.parametrize('name', SINGLE)
+def test_single_signal_golden(name, dtype, engine):
+    g = load_golden(name)
+    m = g['meta']
+    w = make(m['kind'], m['sfreq'], m['interpolate'], m['params'], dtype, engine)
+    fn = {'cwt': w.cwt, 'power': w.power, 'abs': w.abs}[m['op']]
+    got = fn(g['x'], g['freqs'])
+    ref = g['out']
+    assert got.shape == ref.shape
+    if dtype == 'float64':
+        assert got.dtype == ref.dtype
+    t = tol(dtype, m['op'])
+    if m['dtype'] == 'float32':      # the reference ran its forward FFT in single precision
+        t = max(t, 1e-5)
+    assert rel_err(got, ref) <= t, (name, rel_err(got, ref))
+
+
+@pytest.mark.parametrize('name', [n for n in SINGLE if 'w_first' in load_golden(n)])
+def test_device_wavelet_rows_match_reference(name):
+    """The cached rows evaluated by the kernels equal the reference's fft_wavelets."""
+    g = load_golden(name)
+    m = g['meta']
+    w = make(m['kind'], m['sfreq'], m['interpolate'], m['params'], 'float64', None)
+    rows = w.make_fft_wavelets(g['freqs'], m['n'] / m['sfreq'])
+    for got, ref in ((rows[0], g['w_first']), (rows[-1], g['w_last'])):
+        assert got.shape == ref.shape
+        assert np.max(np.abs(got - ref)) <= 1e-13 * max(1.0, np.max(np.abs(ref)))
+
+
+@pytest.mark.parametrize('dtype', ['float64', 'float32'])
+@pytest.mark.parametrize('kind', ['morse', 'morlet', 'shannon', 'mexican_hat'])
+def test_readme_2d_quirk(kind, dtype):
+    """README example with a (1, 300) array: the single cached bin broadcasts."""
+    g = load_golden(f'readme_2d_{kind}')
+    w = make(kind, 1000, False, {}, dtype, None)
+    got = w.power(g['x'], range(1, 100))
+    assert got.shape == g['out'].shape
+    assert np.max(np.abs(got - g['out'])) <= tol(dtype, 'power') * max(1.0, np.max(np.abs(g['out'])))
+
+
+@pytest.mark.parametrize('engine', ENGINES)
+def test_reuse_cache_is_unkeyed(engine):
+    g = load_golden('reuse_morse')
+    w = nw.Morse(1000, engine=engine)
+    assert rel_err(w.cwt(g['xa'], g['freqs']), g['oa']) <= 1e-12
+    assert rel_err(w.cwt(g['xb'], [1., 2.]), g['ob']) <= 1e-12     # freqs ignored, rows padded
+    assert rel_err(w.cwt(g['xc'], None), g['oc']) <= 1e-12         # rows cropped
+    g = load_golden('reuse_morse_interp')
+    w = nw.Morse(1000, interpolate=True, engine=engine)
+    assert rel_err(w.cwt(g['xa'], g['freqs']), g['oa']) <= 1e-12
+    assert rel_err(w.cwt(g['xb'], [1., 2.]), g['ob']) <= 1e-12
+
+
+class FakeEpochs:
+    def __init__(self, data, sfreq, ch_names):
+        self._d, self.info, self.ch_names = data, {'sfreq': sfreq}, list(ch_names)
+
+    def get_data(self):
+        return self._d
+
+
+@pytest.mark.parametrize('dtype', ['float64', 'float32'])
+@pytest.mark.parametrize('kind', ['morse', 'morlet'])
+def test_epochs_wavelet(kind, dtype):
+    g = load_golden(f'epochs_{kind}')
+    ep = FakeEpochs(g['data'], g['meta']['sfreq'], g['meta']['ch_names'])
+    t = TOL[dtype]
+    c = nw.EpochsWavelet(ep, CLASSES[kind](1000, dtype=dtype)).cwt('b', list(g['freqs']))
+    assert c.shape == g['cwt_b'].shape and rel_err(c, g['cwt_b']) <= t
+    p = nw.EpochsWavelet(ep, CLASSES[kind](1000, dtype=dtype)).power('c', list(g['freqs']))
+    assert rel_err(p, g['power_c']) <= 2 * t
+    itc = nw.EpochsWavelet(ep, CLASSES[kind](1000, dtype=dtype)).itc('a', list(g['freqs']))
+    assert rel_err(itc, g['itc_a']) <= (1e-10 if dtype == 'float64' else 1e-3)
+
+
+# ------------------------------------------------------------------ larger sizes
+def synth(S, n, seed, dtype=np.float32, sfreq=1000.):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / sfreq
+    fc = rng.uniform(1, 100, (S, 1))
+    ph = rng.uniform(0, 2 * np.pi, (S, 1))
+    return (np.sin(2 * np.pi * fc * t + ph) + 0.1 * rng.standard_normal((S, n))).astype(dtype)
+
+
+@pytest.mark.parametrize('engine', ENGINES)
+@pytest.mark.parametrize('kind,n,F,dtype', [
+    ('morlet', 16384, 128, 'float32'),     # C2 shape (fewer signals)
+    ('morse', 4096, 256, 'float32'),       # C3 shape
+    ('morse', 16384, 256, 'float32'),      # C4 shape
+    ('morse', 16384, 64, 'float64'),
+    ('shannon', 8192, 16, 'float32'),
+])
+def test_batch_against_oracle_sampled(kind, n, F, dtype, engine):
+    S = 8
+    x = synth(S, n, seed=n + F)
+    freqs = np.arange(1, F + 1, dtype=np.float64)
+    w = CLASSES[kind](1000, dtype=dtype, engine=engine)
+    out = w.cwt_batch(x, freqs)
+    assert out.shape == (S, F, n)
+    rng = np.random.default_rng(1)
+    for s in rng.choice(S, 3, replace=False):
+        fsel = np.sort(rng.choice(F, 6, replace=False))
+        ref = O.cwt(kind, x[s].astype(np.float64), freqs[fsel])
+        assert rel_err(out[s, fsel], ref) <= TOL[dtype] * 3, (s, rel_err(out[s, fsel], ref))
+
+
+@pytest.mark.parametrize('engine', ENGINES)
+def test_power_abs_consistent_and_linear(engine):
+    S, n, F = 16, 4096, 64
+    x = synth(S, n, 5).astype(np.float64)
+    y = synth(S, n, 6).astype(np.float64)
+    freqs = np.linspace(0.5, 200, F)
+    w = nw.Morse(1000, engine=engine)
+    cx = w.cwt_batch(x, freqs)
+    cy = w.cwt_batch(y, freqs)
+    cxy = w.cwt_batch(2.0 * x - 3.0 * y, freqs)
+    assert rel_err(cxy, 2.0 * cx - 3.0 * cy) <= 1e-12
+    assert rel_err(w.cwt_batch(x, freqs, out='power'), np.abs(cx) ** 2) <= 1e-13
+    assert rel_err(w.cwt_batch(x, freqs, out='abs'), np.abs(cx)) <= 1e-13
+    # the batch equals the per-signal drop-in call
+    assert rel_err(cx[3], w.cwt(x[3], freqs)) <= 1e-14
+
+
+def test_engines_agree_fp32():
+    x = synth(32, 16384, 9)
+    freqs = np.arange(1, 65, dtype=np.float64)
+    a = nw.Morse(1000, dtype='float32', engine='rocfft').cwt_batch(x, freqs, out='power')
+    b = nw.Morse(1000, dtype='float32').cwt_batch(x, freqs, out='power')
+    assert rel_err(b, a) <= 2e-5
+
+
+def test_empty_and_ragged_inputs():
+    w = nw.Morse(1000)
+    out = w.cwt_batch(np.zeros((0, 256)), [1., 2., 3.])
+    assert out.shape == (0, 3, 256)
+    for n in (1, 2, 3, 5, 127, 1000, 1021):
+        x = synth(1, n, n)[0].astype(np.float64)
+        ref = O.cwt('morse', x, [2., 7., 30.])
+        got = nw.Morse(1000).cwt(x, [2., 7., 30.])
+        assert rel_err(got, ref) <= 1e-12, n
+
+
+def test_device_tensors_and_streams():
+    torch = pytest.importorskip('torch')
+    n, F, S = 16384, 32, 8
+    x = synth(S, n, 11)
+    plan = nw.Plan(n, F, 'float32', device=0, max_batch=S)
+    g = nw._lib.trans_grid(n / 1000., 1000., False)
+    plan.set_wavelet('morse', [17.5, 3.], np.arange(1, F + 1, dtype=np.float64), g)
+    host = plan.execute(x, out_kind='cwt')
+    xt = torch.from_numpy(x).cuda()
+    ot = torch.empty((S, F, n), dtype=torch.complex64, device='cuda')
+    plan.execute(xt, ot, out_kind='cwt')
+    plan.sync()
+    np.testing.assert_array_equal(ot.cpu().numpy(), host)
+
+
+def test_multi_plan_sharding_is_exact():
+    n, F, S = 4096, 16, 10
+    x = synth(S, n, 12)
+    g = nw._lib.trans_grid(n / 1000., 1000., False)
+    freqs = np.arange(1, F + 1, dtype=np.float64)
+    plans = []
+    for _ in range(2):                               # two shards on device 0
+        p = nw.Plan(n, F, 'float32', device=0, max_batch=8)
+        p.set_wavelet('morse', [17.5, 3.], freqs, g)
+        plans.append(p)
+    single = plans[0].execute(x, out_kind='power')
+    sharded = nw.execute_multi(plans, x, out_kind='power')
+    np.testing.assert_array_equal(sharded, single)

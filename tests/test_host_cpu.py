@@ -1,0 +1,131 @@
+"""CPU-only checks of the boundary and the host logic (no GPU needed)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, golden_names, load_golden
+from oracle import nw_oracle as O
+
+import ninwavelets_amd as nw
+from ninwavelets_amd import _lib as L
+
+
+def header_functions():
+    text = open(os.path.join(ROOT, 'include', 'ninwave.h')).read()
+    text = re.sub(r'/\*.*?\*/', '', text, flags=re.S)
+    return sorted(set(re.findall(r'\b(nw_[a-z_]+)\s*\(', text)))
+
+
+def test_library_exports_every_header_symbol():
+    lib = L.lib()
+    names = header_functions()
+    assert len(names) >= 14
+    for name in names:
+        assert hasattr(lib, name), name
+    # and the ctypes table binds exactly the header's functions
+    assert sorted(n for n, _, _ in L.SIGNATURES) == names
+
+
+def test_version_and_no_device_here():
+    assert L.lib().nw_version().startswith(b'ninwave')
+    if not os.path.exists('/dev/kfd'):
+        assert L.device_count() == 0
+
+
+@pytest.mark.skipif(os.path.exists('/dev/kfd'), reason='a GPU is present')
+def test_no_cpu_fallback_without_gpu():
+    with pytest.raises(L.NinwaveError):
+        nw.Plan(256, 4, 'float32')
+    with pytest.raises(L.NinwaveError):
+        nw.Morse(1000).cwt(np.zeros(256), [1., 2.])
+
+
+@pytest.mark.parametrize('interp', [False, True])
+@pytest.mark.parametrize('sfreq', [1000., 500., 256., 1024., 333.3, 44100.])
+def test_trans_grid_matches_numpy_arange(sfreq, interp):
+    """nw_trans_grid restates _setup_trans_shape + hstack + interpolate_alias
+    (base.py:173-194, 238-246, 274-276) bit for bit, including the N+1 lengths."""
+    for n in list(range(1, 700)) + [1023, 1024, 4096, 4097, 16384, 1 << 20, 1 << 24]:
+        rl = n / sfreq
+        g = L.trans_grid(rl, sfreq, interp)
+        t = O.trans_grid(sfreq, rl, interp)
+        assert g.len_valid == t.shape[0], (n, sfreq)
+        assert g.len_full == (2 * t.shape[0] if interp else t.shape[0])
+        assert g.delta == 1 / rl
+        if t.shape[0] > 1:
+            assert t[1] == g.delta and t[-1] == (t.shape[0] - 1) * g.delta
+
+
+def test_trans_grid_arbitrary_real_length():
+    for rl in [1.0, 0.5, 2.5, 1e-3, 7.123]:
+        g = L.trans_grid(rl, 1000., False)
+        assert g.len_full == O.trans_grid(1000., rl, False).shape[0]
+
+
+def test_trans_grid_rejects_bad_args():
+    with pytest.raises(ValueError):
+        L.trans_grid(0.0, 1000., False)
+    with pytest.raises(ValueError):
+        L.trans_grid(1.0, -1., False)
+
+
+def test_fused_support_table():
+    assert L.fused_supported(300, L.NW_F32) is False        # non power of two -> rocFFT engine
+
+
+# ---------------------------------------------------------------- host-side errors
+def test_errors_match_reference_before_any_device_call():
+    m = nw.Morse(1000)
+    with pytest.raises(IndexError):
+        m.cwt(np.zeros(64), [5.])                   # freqs[1] (base.py:272)
+    with pytest.raises(ZeroDivisionError):
+        nw.Morse(1000).cwt(np.zeros(64), [0., 1.])  # base.py:234-235
+    with pytest.raises(TypeError):
+        nw.Morse(1000).cwt(np.zeros(64), None)       # None[1]
+    with pytest.raises(ZeroDivisionError):
+        nw.MexicanHat(1000).cwt(np.zeros(64), [0., 1.])
+
+
+# ---------------------------------------------------------------- host table builds
+@pytest.mark.parametrize('name', [n for n in golden_names() if n.startswith(('mexhat', 'haar'))])
+def test_normal_mode_table_rows_match_reference(name):
+    g = load_golden(name)
+    if 'w_first' not in g:
+        pytest.skip('no rows stored')
+    m = g['meta']
+    cls = nw.MexicanHat if m['kind'] == 'mexican_hat' else nw.Haar
+    w = cls(m['sfreq'], interpolate=m['interpolate'])
+    cache = w._build_cache(g['freqs'], m['n'] / m['sfreq'])
+    np.testing.assert_array_equal(cache.table[0], g['w_first'])
+    np.testing.assert_array_equal(cache.table[-1], g['w_last'])
+
+
+def test_plugin_subclass_becomes_table():
+    class Sq(nw.Morse):
+        def trans_formula(self, freqs, freq=1.):
+            return np.exp(-(freqs - freq) ** 2)
+
+    w = Sq(1000)
+    c = w._build_cache([5., 10., 20.], 256 / 1000)
+    assert c.kind == 'table' and c.table.shape == (3, 256)
+    t = np.arange(0, 1000 / (256 / 1000) * (256 / 1000), 1 / (256 / 1000))
+    np.testing.assert_array_equal(c.table[1].real, np.exp(-(t - 10.) ** 2))
+    assert nw.Morse(1000)._build_cache([5., 10.], 0.256).kind == 'morse'
+
+
+def test_reference_api_surface():
+    for name in ['WaveletBase', 'WaveletMode', 'Morse', 'MorseMNE', 'Morlet', 'Haar',
+                 'MexicanHat', 'Shannon', 'EpochsWavelet']:
+        assert hasattr(nw, name)
+    m = nw.Morse(1000, b=17.5, r=3)
+    assert (m.b, m.r, m.mode, m.sfreq, m.interpolate) == (17.5, 3, nw.WaveletMode.Reverse, 1000, False)
+    assert nw.Morlet().mode == nw.WaveletMode.Both
+    assert nw.MexicanHat().mode == nw.WaveletMode.Normal
+    assert nw.WaveletBase().interpolate is True
+    # the numpy plugin formulas equal the oracle's restatement
+    nu = np.linspace(0, 500, 1001)
+    np.testing.assert_array_equal(nw.Morse().trans_formula(nu, 40.), O.morse_spectrum(nu, 40.))
+    np.testing.assert_array_equal(nw.Morlet().trans_formula(nu, 40.), O.morlet_spectrum(nu, 40.))

@@ -1,0 +1,63 @@
+"""Pin the CPU oracle (oracle/nw_oracle.py) against vectors produced by the
+reference itself (tests/golden/make_golden.py).  Bit-exact is expected: the
+oracle performs the same numpy/scipy.fftpack operations in the same order."""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden
+from oracle import nw_oracle as O
+
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs'))]
+
+
+def _params(meta):
+    p = dict(meta['params'])
+    p.pop('real_wave_length', None)
+    return p
+
+
+@pytest.mark.parametrize('name', SINGLE)
+def test_oracle_matches_reference(name):
+    g = load_golden(name)
+    m = g['meta']
+    kw = dict(sfreq=m['sfreq'], interpolate=m['interpolate'], **_params(m))
+    if m['op'] == 'cwt':
+        got = O.cwt(m['kind'], g['x'], g['freqs'], **kw)
+    elif m['op'] == 'power':
+        got = O.power(m['kind'], g['x'], g['freqs'], **kw)
+    else:
+        got = np.abs(O.cwt(m['kind'], g['x'], g['freqs'], **kw))
+    ref = g['out']
+    assert got.shape == ref.shape and got.dtype == ref.dtype
+    assert np.max(np.abs(got - ref)) <= 1e-15 * max(1.0, np.max(np.abs(ref)))
+    if 'w_first' in g:
+        rows = O.fft_wavelets(m['kind'], g['freqs'], m['sfreq'], m['n'] / m['sfreq'],
+                              m['interpolate'], **_params(m))
+        np.testing.assert_array_equal(rows[0], g['w_first'])
+        np.testing.assert_array_equal(rows[-1], g['w_last'])
+
+
+@pytest.mark.parametrize('kind', ['morse', 'morlet'])
+def test_oracle_epochs(kind):
+    g = load_golden(f'epochs_{kind}')
+    data = g['data']
+    sf = g['meta']['sfreq']
+    np.testing.assert_allclose(O.epochs_cwt(kind, data[:, 1, :], g['freqs'], sfreq=sf),
+                               g['cwt_b'], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(O.epochs_power(kind, data[:, 2, :], g['freqs'], sfreq=sf),
+                               g['power_c'], rtol=0, atol=1e-15)
+    np.testing.assert_allclose(O.epochs_itc(kind, data[:, 0, :], g['freqs'], sfreq=sf),
+                               g['itc_a'], rtol=0, atol=1e-15)
+
+
+def test_oracle_reuse_quirk():
+    g = load_golden('reuse_morse')
+    rows = O.fft_wavelets('morse', g['freqs'], 1000., 300 / 1000., False)
+    np.testing.assert_array_equal(O.cwt_from_rows(g['xa'], rows, False), g['oa'])
+    np.testing.assert_array_equal(O.cwt_from_rows(g['xb'], rows, False), g['ob'])
+    np.testing.assert_array_equal(O.cwt_from_rows(g['xc'], rows, False), g['oc'])
+
+
+def test_oracle_make_example_matches_fixture_input():
+    g = load_golden('example_morse_power')
+    np.testing.assert_array_equal(O.make_example(1.0), g['x'])
