@@ -113,9 +113,14 @@ int nw_plan_create(nw_plan** plan, int device, int64_t n, int64_t max_batch,
  *   the cache and pad_to's it to the current n).
  *   params: NW_MORSE {b, r}; NW_MORLET {sigma, gabor[, c, k]} (c, k of wavelets.py:118-122,
  *   derived from sigma when absent); NW_SHANNON {}; NW_TABLE {}.
- *   table: NW_TABLE only, complex128 [nfreq][grid.len_full], copied to the device. */
+ *   table: NW_TABLE only, complex128 [nfreq][grid.len_full], copied to the device.
+ *   row_len: NW_TABLE only, optional [nfreq] true length of each row (rows are
+ *   left-aligned in the table); the reference pad_to's every row on its own
+ *   (base.py:396-397) and time-domain rows can differ by one sample.  NULL: all
+ *   rows are grid.len_full long. */
 int nw_plan_set_wavelet(nw_plan* plan, int kind, const double* params, int nparams,
-                        const double* freqs, const nw_grid* grid, const void* table);
+                        const double* freqs, const nw_grid* grid, const void* table,
+                        const int64_t* row_len);
 
 /* Evaluate the attached wavelet rows on the device and copy them to the host:
  * out[nfreq][grid.len_full] of the plan dtype (real for analytic kinds, complex

@@ -3,6 +3,10 @@
 The shared library is built in-tree by ``__graft_entry__.build()`` (or
 ``make -C ninwavelets_amd/csrc``).  There is no fallback: if the library is
 missing or a GPU is absent, calls raise instead of computing on the CPU.
+
+Mixing with PyTorch in one process: torch wheels bundle their own HIP runtime.
+Import torch BEFORE this package, so libninwave.so binds to torch's already
+loaded libamdhip64/librocfft (same sonames) and the process keeps one runtime.
 """
 from __future__ import annotations
 
@@ -59,7 +63,8 @@ SIGNATURES = [
     ('nw_plan_create', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _I64, _I64, ctypes.c_int32,
                                       ctypes.c_int, ctypes.c_uint32]),
     ('nw_plan_set_wavelet', ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
-                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(nw_grid), _P]),
+                                           ctypes.POINTER(ctypes.c_double), ctypes.POINTER(nw_grid), _P,
+                                           ctypes.POINTER(ctypes.c_int64)]),
     ('nw_plan_wavelet_rows', ctypes.c_int, [_P, _P]),
     ('nw_execute', ctypes.c_int, [_P, _P, _I64, _P, ctypes.c_int, ctypes.c_int]),
     ('nw_execute_multi', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),

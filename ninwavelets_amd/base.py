@@ -60,10 +60,13 @@ class _Cache:
 
     _version = 0
 
-    def __init__(self, kind, params, freqs, grid, table=None):
+    def __init__(self, kind, params, freqs, grid, table=None, row_len=None):
         _Cache._version += 1
         self.version = _Cache._version
         self.kind, self.params, self.freqs, self.grid, self.table = kind, params, freqs, grid, table
+        if row_len is None and table is not None:
+            row_len = np.full(table.shape[0], table.shape[1], dtype=np.int64)
+        self.row_len = row_len
 
 
 class WaveletBase:
@@ -186,13 +189,14 @@ class WaveletBase:
 
     @staticmethod
     def _table_cache(rows, freqs) -> _Cache:
-        lens = {np.asarray(r).shape[0] for r in rows}
-        if len(lens) != 1:
-            raise ValueError('all cached wavelet rows must have the same length')
-        table = np.ascontiguousarray(np.array(rows), dtype=np.complex128)
-        m = table.shape[1]
+        rows = [np.asarray(r) for r in rows]
+        lens = np.array([r.shape[0] for r in rows], dtype=np.int64)
+        m = int(lens.max()) if len(rows) else 0
+        table = np.zeros((len(rows), m), dtype=np.complex128)   # rows left-aligned
+        for i, r in enumerate(rows):
+            table[i, :r.shape[0]] = r
         grid = L.nw_grid(1.0, m, m)
-        return _Cache('table', [], freqs, grid, table)
+        return _Cache('table', [], freqs, grid, table, lens)
 
     def make_fft_wavelets(self, freqs, real_wave_length: float = 1.) -> list:
         """Build (and return) the cached rows (base.py:258-279)."""
@@ -208,7 +212,7 @@ class WaveletBase:
             raise AttributeError('fft_wavelets')
         if self._rows is None:
             if c.kind == 'table':
-                self._rows = [row for row in c.table]
+                self._rows = [row[:n] for row, n in zip(c.table, c.row_len)]
             else:
                 plan = Plan(max(1, c.grid.len_full), len(c.freqs), 'float64', self.device)
                 plan.set_wavelet(c.kind, c.params, c.freqs, c.grid)
@@ -245,7 +249,8 @@ class WaveletBase:
             plan = Plan(n, nf, self.dtype, device, batch, self.interpolate, self.engine)
             self._plans[key] = plan
         if plan.wavelet_token != c.version:
-            plan.set_wavelet(c.kind, c.params, c.freqs, c.grid, c.table, token=c.version)
+            plan.set_wavelet(c.kind, c.params, c.freqs, c.grid, c.table, token=c.version,
+                             row_len=c.row_len)
         return plan
 
     def _run(self, x: np.ndarray, out_kind: str) -> np.ndarray:

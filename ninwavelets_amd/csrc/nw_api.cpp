@@ -91,6 +91,7 @@ struct nw_plan {
     double* d_peak = nullptr;
     float* d_xstep32 = nullptr;
     void* d_table = nullptr;
+    int64_t* d_row_len = nullptr;
 
     // buffers
     void* d_x = nullptr;
@@ -262,7 +263,8 @@ void free_plan(nw_plan* p) {
     for (auto& kv : p->fwd) rocfft_plan_destroy(kv.second);
     for (auto& kv : p->inv) rocfft_plan_destroy(kv.second);
     if (p->info) rocfft_execution_info_destroy(p->info);
-    void* bufs[] = {p->work, p->d_x, p->d_X, p->d_Y, p->d_out, p->d_freq, p->d_peak, p->d_xstep32, p->d_table};
+    void* bufs[] = {p->work,   p->d_x,    p->d_X,        p->d_Y,     p->d_out,
+                    p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& pe : p->pending) {
@@ -386,7 +388,7 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
 }
 
 int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams, const double* freqs,
-                        const nw_grid* grid, const void* table) {
+                        const nw_grid* grid, const void* table, const int64_t* row_len) {
     if (!p || !freqs || !grid) return fail(NW_E_INVALID, "nw_plan_set_wavelet: null argument");
     if (kind < NW_MORSE || kind > NW_TABLE) return fail(NW_E_INVALID, "nw_plan_set_wavelet: unknown kind");
     if (kind == NW_TABLE && !table) return fail(NW_E_INVALID, "nw_plan_set_wavelet: NW_TABLE needs a table");
@@ -437,6 +439,21 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
         NW_HIP(hipFree(p->d_table));
         p->d_table = nullptr;
     }
+    if (p->d_row_len) {
+        NW_HIP(hipFree(p->d_row_len));
+        p->d_row_len = nullptr;
+    }
+    if (kind == NW_TABLE) {
+        std::vector<int64_t> rl(F, grid->len_full);
+        if (row_len)
+            for (int i = 0; i < F; ++i) {
+                if (row_len[i] < 0 || row_len[i] > grid->len_full)
+                    return fail(NW_E_INVALID, "nw_plan_set_wavelet: row_len out of range");
+                rl[i] = row_len[i];
+            }
+        NW_HIP(hipMalloc((void**)&p->d_row_len, F * sizeof(int64_t)));
+        NW_HIP(hipMemcpy(p->d_row_len, rl.data(), F * sizeof(int64_t), hipMemcpyHostToDevice));
+    }
     if (kind == NW_TABLE && grid->len_full > 0) {
         const size_t cnt = (size_t)F * grid->len_full;
         const size_t bytes = cnt * 2 * p->esz;
@@ -454,6 +471,7 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
     d.peak = p->d_peak;
     d.xstep32 = p->d_xstep32;
     d.table = p->d_table;
+    d.row_len = p->d_row_len;
     p->desc = d;
     p->has_wavelet = true;
     return NW_OK;

@@ -34,43 +34,21 @@ template <typename T> __device__ __forceinline__ C2<T> cmul(C2<T> a, C2<T> b) {
     return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
 
-// --- buffer (SRD) memory ops: a wave-uniform 128-bit descriptor in SGPRs plus a
-// 32-bit per-lane byte offset (cdna_hip_programming.md T8/T20) instead of a
-// 64-bit address per access.
-using rsrc_t = __amdgpu_buffer_rsrc_t;
-__device__ __forceinline__ rsrc_t make_rsrc(const void* base, uint32_t bytes) {
-    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+// --- memory ops addressed as wave-uniform base (SGPR pair) + 32-bit per-lane byte
+// offset: `global_load/store ... v_off, s[base:base+1]` (saddr form), i.e. one VGPR
+// per address instead of a 64-bit pair.  The empty asm makes the offset opaque so
+// the compiler cannot re-associate constant parts back into 64-bit address math.
+// (The raw_buffer_load/store_b64 builtins of this toolchain emit a single dword
+// and are not used.)
+template <typename P>
+__device__ __forceinline__ P* at(P* base, uint32_t byte_off) {
+    asm("" : "+v"(byte_off));
+    return reinterpret_cast<P*>(reinterpret_cast<char*>(base) + byte_off);
 }
-__device__ __forceinline__ C2<float> bload(rsrc_t r, uint32_t off, C2<float>*) {
-    auto u = __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0);
-    return {__builtin_bit_cast(float, u[0]), __builtin_bit_cast(float, u[1])};
-}
-__device__ __forceinline__ C2<double> bload(rsrc_t r, uint32_t off, C2<double>*) {
-    auto u = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
-    const uint64_t lo = ((uint64_t)u[1] << 32) | u[0], hi = ((uint64_t)u[3] << 32) | u[2];
-    return {__builtin_bit_cast(double, lo), __builtin_bit_cast(double, hi)};
-}
-template <typename T> __device__ __forceinline__ C2<T> bload_c(rsrc_t r, uint32_t off) {
-    return bload(r, off, (C2<T>*)nullptr);
-}
-__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, C2<float> y) {
-    __attribute__((ext_vector_type(2))) unsigned int u = {__builtin_bit_cast(unsigned int, y.re),
-                                                         __builtin_bit_cast(unsigned int, y.im)};
-    __builtin_amdgcn_raw_buffer_store_b64(u, r, off, 0, 0);
-}
-__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, C2<double> y) {
-    const uint64_t a = __builtin_bit_cast(uint64_t, y.re), b = __builtin_bit_cast(uint64_t, y.im);
-    __attribute__((ext_vector_type(4))) unsigned int u = {(unsigned)a, (unsigned)(a >> 32), (unsigned)b,
-                                                         (unsigned)(b >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b128(u, r, off, 0, 0);
-}
-__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, float y) {
-    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned int, y), r, off, 0, 0);
-}
-__device__ __forceinline__ void bstore(rsrc_t r, uint32_t off, double y) {
-    const uint64_t a = __builtin_bit_cast(uint64_t, y);
-    __attribute__((ext_vector_type(2))) unsigned int u = {(unsigned)a, (unsigned)(a >> 32)};
-    __builtin_amdgcn_raw_buffer_store_b64(u, r, off, 0, 0);
+template <typename P>
+__device__ __forceinline__ const P* at(const P* base, uint32_t byte_off) {
+    asm("" : "+v"(byte_off));
+    return reinterpret_cast<const P*>(reinterpret_cast<const char*>(base) + byte_off);
 }
 
 // cos(2*pi*i/32), i = 0..31
@@ -148,12 +126,12 @@ template <int R> constexpr int ilog2() { return R <= 1 ? 0 : 1 + ilog2<R / 2>();
 // come from the exact table tw[i] = exp(2 pi i i / N) (L2-resident); every other
 // power is a product of at most log2(R) of them: a few ulp, no recurrence drift.
 template <typename T, int R, int N, int NSR>
-__device__ __forceinline__ void twiddle(C2<T>* v, int m, rsrc_t tw) {
+__device__ __forceinline__ void twiddle(C2<T>* v, int m, const C2<T>* __restrict__ tw) {
     if constexpr (R > 1) {
         constexpr int LR = ilog2<R>();
         C2<T> p[LR];
 #pragma unroll
-        for (int k = 0; k < LR; ++k) p[k] = bload_c<T>(tw, (uint32_t)((m << k) * (N / NSR)) * sizeof(C2<T>));
+        for (int k = 0; k < LR; ++k) p[k] = *at(tw, (uint32_t)((m << k) * (N / NSR) * sizeof(C2<T>)));
 #pragma unroll
         for (int r = 1; r < R; ++r) {
             C2<T> w = p[__builtin_ctz(r)];
@@ -191,15 +169,15 @@ template <int N, int E> struct Geometry {
     }
 };
 
-// one output point of the current row (descriptor based at the row start)
+// one output point of the current row (orow = wave-uniform row base)
 template <int OUT, typename T>
-__device__ __forceinline__ void store_out(rsrc_t orow, uint32_t idx, C2<T> y) {
+__device__ __forceinline__ void store_out(void* orow, uint32_t idx, C2<T> y) {
     if constexpr (OUT == NW_OUT_CWT) {
-        bstore(orow, idx * (uint32_t)sizeof(C2<T>), y);
+        *at(reinterpret_cast<C2<T>*>(orow), idx * (uint32_t)sizeof(C2<T>)) = y;
     } else if constexpr (OUT == NW_OUT_POWER) {
-        bstore(orow, idx * (uint32_t)sizeof(T), y.re * y.re + y.im * y.im);
+        *at(reinterpret_cast<T*>(orow), idx * (uint32_t)sizeof(T)) = y.re * y.re + y.im * y.im;
     } else {
-        bstore(orow, idx * (uint32_t)sizeof(T), (T)sqrt(y.re * y.re + y.im * y.im));
+        *at(reinterpret_cast<T*>(orow), idx * (uint32_t)sizeof(T)) = (T)sqrt(y.re * y.re + y.im * y.im);
     }
 }
 
@@ -208,7 +186,8 @@ __device__ __forceinline__ void store_out(rsrc_t orow, uint32_t idx, C2<T> y) {
 // lds_idx(a + c) = lds_idx(a) + c + c/32 whenever c is a multiple of 32, and for
 // NS < 32 the pad of d0 + r*NS splits into a per-thread and a per-r part.
 template <typename T, int N, int E, int P, int OUT>
-__device__ __forceinline__ void stockham_pass(C2<T>* v, C2<T>* lds, int t, rsrc_t orow, rsrc_t tw) {
+__device__ __forceinline__ void stockham_pass(C2<T>* v, C2<T>* lds, int t, void* orow,
+                                              const C2<T>* __restrict__ tw) {
     using G = Geometry<N, E>;
     constexpr int R = G::radix(P);
     constexpr int NS = G::ns(P);
@@ -252,7 +231,8 @@ __device__ __forceinline__ void stockham_pass(C2<T>* v, C2<T>* lds, int t, rsrc_
 }
 
 template <typename T, int N, int E, int OUT, int P>
-__device__ __forceinline__ void run_passes(C2<T>* v, C2<T>* lds, int t, rsrc_t orow, rsrc_t tw) {
+__device__ __forceinline__ void run_passes(C2<T>* v, C2<T>* lds, int t, void* orow,
+                                           const C2<T>* __restrict__ tw) {
     using G = Geometry<N, E>;
     if constexpr (P < G::npass()) {
         stockham_pass<T, N, E, P, OUT>(v, lds, t, orow, tw);
@@ -295,15 +275,13 @@ __global__ __launch_bounds__(N / E) void nw_fused_kernel(WDesc d, const cplx<T>*
     const int64_t s_begin = (int64_t)sg * group;
     const int64_t s_end = min(nsig, s_begin + group);
 
-    const rsrc_t twr = make_rsrc(tw, (uint32_t)(N * sizeof(C2<T>)));
-
     // 1. wavelet bins of this thread, evaluated once per block (1/n folded in)
     WReg<T, REALW> w[E];
 #pragma unroll
     for (int r = 0; r < E; ++r) w[r].set(wavelet_bin<T>(d, fi, t + r * G::T));
 
     for (int64_t s = s_begin; s < s_end; ++s) {
-        const rsrc_t xs = make_rsrc(X + s * d.nh, (uint32_t)(d.nh * sizeof(C2<T>)));
+        const C2<T>* xs = reinterpret_cast<const C2<T>*>(X + s * d.nh);
         C2<T> v[E];
         // 2. pass 0 (Ns = 1): z = W * X at k = t + r*T, radix-E IDFT in registers.
         //    k < N/2 exactly when r < E/2 (compile-time), so the half-spectrum read
@@ -313,9 +291,9 @@ __global__ __launch_bounds__(N / E) void nw_fused_kernel(WDesc d, const cplx<T>*
         for (int r = 0; r < E; ++r) {
             C2<T> x;
             if (r < E / 2) {
-                x = bload_c<T>(xs, (uint32_t)(t + r * G::T) * (uint32_t)sizeof(C2<T>));
+                x = *at(xs, (uint32_t)(t + r * G::T) * (uint32_t)sizeof(C2<T>));
             } else {
-                x = bload_c<T>(xs, (uint32_t)(N - t - r * G::T) * (uint32_t)sizeof(C2<T>));
+                x = *at(xs, (uint32_t)(N - t - r * G::T) * (uint32_t)sizeof(C2<T>));
                 x.im = -x.im;
             }
             const bool keep = t + r * G::T < d.xlim;     // interpolate_alias mask
@@ -331,9 +309,8 @@ __global__ __launch_bounds__(N / E) void nw_fused_kernel(WDesc d, const cplx<T>*
         }
         __syncthreads();
         const int64_t row = (s * d.nfreq + fi) * (int64_t)N;
-        const rsrc_t orow = make_rsrc((const char*)out + row * (OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T)),
-                                      (uint32_t)(N * (OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T))));
-        run_passes<T, N, E, OUT, 1>(v, lds, t, orow, twr);
+        void* orow = (char*)out + row * (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T));
+        run_passes<T, N, E, OUT, 1>(v, lds, t, orow, tw);
         __syncthreads();   // the last pass's LDS reads finish before the next signal's scatter
     }
 }

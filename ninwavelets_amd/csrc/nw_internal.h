@@ -37,6 +37,7 @@ struct WDesc {
     const double* peak;      // Morlet p(f) = sigma / (1 - exp(-sigma f))
     const float*  xstep32;   // fp32 path: (float)(delta / f)  (Morse) or (float)(delta / f * p(f)) (Morlet)
     const void*   table;     // NW_TABLE: complex[nfreq][len_full] of the plan dtype
+    const int64_t* row_len;  // NW_TABLE: true length of each (left-aligned) row
 };
 
 template <typename T> struct cplx { T re, im; };
@@ -87,16 +88,19 @@ template <> __device__ __forceinline__ float  psi<float >(const WDesc& d, int fi
 // W[f, k] for output bin k (scaled by 1/n), complex in general (TABLE rows).
 template <typename T>
 __device__ __forceinline__ cplx<T> wavelet_bin(const WDesc& d, int fi, int64_t k) {
-    const int64_t j = k - d.off;
     cplx<T> w{T(0), T(0)};
-    if (j >= 0 && j < d.len_valid) {
-        if (d.kind == NW_TABLE) {
+    if (d.kind == NW_TABLE) {
+        // every row is pad_to'd on its own (rows may differ in length)
+        const int64_t len = d.row_len[fi];
+        const int64_t j = k - (len < d.n ? (d.n - len) / 2 : 0);
+        if (j >= 0 && j < len) {
             const cplx<T> t = reinterpret_cast<const cplx<T>*>(d.table)[(int64_t)fi * d.len_full + j];
             w.re = t.re * (T)d.scale;
             w.im = t.im * (T)d.scale;
-        } else {
-            w.re = psi<T>(d, fi, j) * (T)d.scale;
         }
+    } else {
+        const int64_t j = k - d.off;
+        if (j >= 0 && j < d.len_valid) w.re = psi<T>(d, fi, j) * (T)d.scale;
     }
     return w;
 }

@@ -109,7 +109,7 @@ __global__ __launch_bounds__(256) void k_rows(WDesc d, T* __restrict__ rows) {
     if (j >= d.len_full) return;
     if (d.kind == NW_TABLE) {
         const cplx<T>* t = reinterpret_cast<const cplx<T>*>(d.table) + (int64_t)fi * d.len_full;
-        reinterpret_cast<cplx<T>*>(rows)[(int64_t)fi * d.len_full + j] = t[j];
+        reinterpret_cast<cplx<T>*>(rows)[(int64_t)fi * d.len_full + j] = j < d.row_len[fi] ? t[j] : cplx<T>{T(0), T(0)};
     } else {
         rows[(int64_t)fi * d.len_full + j] = j < d.len_valid ? psi<T>(d, fi, j) : T(0);
     }

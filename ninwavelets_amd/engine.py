@@ -60,20 +60,24 @@ class Plan:
         self.wavelet_token = None
 
     # -- wavelet -----------------------------------------------------------------
-    def set_wavelet(self, kind: str, params, freqs, grid: L.nw_grid, table=None, token=None):
+    def set_wavelet(self, kind: str, params, freqs, grid: L.nw_grid, table=None, token=None,
+                    row_len=None):
         freqs = np.ascontiguousarray(freqs, dtype=np.float64)
         if freqs.shape != (self.nfreq,):
             raise ValueError(f'expected {self.nfreq} freqs, got {freqs.shape}')
         p = np.ascontiguousarray(params if params is not None else [], dtype=np.float64)
-        tab_ptr = None
+        tab_ptr = rl_ptr = None
         if KINDS[kind] == L.NW_TABLE:
             table = np.ascontiguousarray(table, dtype=np.complex128)
             if table.shape != (self.nfreq, grid.len_full):
                 raise ValueError(f'table must be ({self.nfreq}, {grid.len_full}), got {table.shape}')
             tab_ptr = table.ctypes.data_as(ctypes.c_void_p)
+            if row_len is not None:
+                row_len = np.ascontiguousarray(row_len, dtype=np.int64)
+                rl_ptr = row_len.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))
         L.check(L.lib().nw_plan_set_wavelet(
             self._h, KINDS[kind], p.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(p.size),
-            freqs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(grid), tab_ptr))
+            freqs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(grid), tab_ptr, rl_ptr))
         self.kind, self.grid = kind, grid
         self.wavelet_token = token
 

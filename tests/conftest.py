@@ -6,6 +6,15 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# torch wheels bundle their own HIP runtime (libamdhip64.so, librocfft.so).  When
+# torch is loaded first, libninwave.so binds to that same runtime (matching
+# sonames); loaded the other way round the process would hold two HIP runtimes.
+# So the suite imports torch first, exactly as bench.py does.
+try:
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the product
+    torch = None
 GOLDEN = os.path.join(ROOT, 'tests', 'golden')
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
