@@ -100,6 +100,9 @@ struct nw_plan {
     size_t d_Y_bytes = 0;
     void* d_out = nullptr;
     size_t d_out_bytes = 0;
+    void* d_wtab = nullptr;          // fused engine: W[f, k] (pad_to + 1/n applied)
+    size_t d_wtab_bytes = 0;
+    bool wtab_valid = false;
 
     // rocFFT, keyed by batch count
     std::map<int64_t, rocfft_plan> fwd, inv;
@@ -231,8 +234,14 @@ int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind
     NW_TRY(staged(p, ST_FWD, [&] { return run_fft(p, fwd, p->d_x, p->d_X); }));
 
     if (!rocfft_engine) {
+        if (!p->wtab_valid) {
+            NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes,
+                          nw::fused_wtable_bytes(p->n, p->nfreq, p->dtype, p->desc.kind)));
+            NW_HIP(nw::build_wtable(p->desc, p->dtype, p->d_wtab, p->stream));
+            p->wtab_valid = true;
+        }
         return staged(p, ST_FUSED, [&] {
-            NW_HIP(nw::launch_fused(p->desc, p->dtype, out_kind, p->d_X, dst, c, p->stream));
+            NW_HIP(nw::launch_fused(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->stream));
             return NW_OK;
         });
     }
@@ -263,7 +272,7 @@ void free_plan(nw_plan* p) {
     for (auto& kv : p->fwd) rocfft_plan_destroy(kv.second);
     for (auto& kv : p->inv) rocfft_plan_destroy(kv.second);
     if (p->info) rocfft_execution_info_destroy(p->info);
-    void* bufs[] = {p->work,   p->d_x,    p->d_X,        p->d_Y,     p->d_out,
+    void* bufs[] = {p->work,   p->d_x,    p->d_X,        p->d_Y,     p->d_out,      p->d_wtab,
                     p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -474,6 +483,7 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
     d.row_len = p->d_row_len;
     p->desc = d;
     p->has_wavelet = true;
+    p->wtab_valid = false;
     return NW_OK;
 }
 

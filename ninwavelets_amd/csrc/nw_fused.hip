@@ -143,8 +143,14 @@ __device__ __forceinline__ void twiddle(C2<T>* v, int m, const C2<T>* __restrict
     }
 }
 
-// padded LDS image: one extra element every 32 keeps the Ns=1 scatter conflict-free
-__device__ __forceinline__ int lds_idx(int i) { return i + (i >> 5); }
+// Padded LDS half image (one real component at a time): 2 extra slots after
+// every E slots (E = elements per thread).  The pass-0 scatter (thread t owns
+// slots t*E .. t*E+E-1) then hits distinct banks with pair stores, pairs stay
+// aligned, and every later access is base(thread) + compile-time offset because
+// all strides are multiples of E.
+template <int E> __device__ __forceinline__ int lds_idx(int i) { return i + 2 * (i / E); }
+template <int E> constexpr int lds_off(int c) { return c + 2 * (c / E); }   // c a multiple of E
+template <int N, int E> constexpr int lds_elems() { return N + 2 * (N / E); }
 
 template <int N, int E> struct Geometry {
     static constexpr int T = N / E;                 // threads per block
@@ -169,98 +175,173 @@ template <int N, int E> struct Geometry {
     }
 };
 
-// one output point of the current row (orow = wave-uniform row base)
+// output value of one point: y, |y| or |y|^2
+template <int OUT, typename T> struct OutT { using type = T; };
+template <typename T> struct OutT<NW_OUT_CWT, T> { using type = C2<T>; };
 template <int OUT, typename T>
-__device__ __forceinline__ void store_out(void* orow, uint32_t idx, C2<T> y) {
-    if constexpr (OUT == NW_OUT_CWT) {
-        *at(reinterpret_cast<C2<T>*>(orow), idx * (uint32_t)sizeof(C2<T>)) = y;
-    } else if constexpr (OUT == NW_OUT_POWER) {
-        *at(reinterpret_cast<T*>(orow), idx * (uint32_t)sizeof(T)) = y.re * y.re + y.im * y.im;
-    } else {
-        *at(reinterpret_cast<T*>(orow), idx * (uint32_t)sizeof(T)) = (T)sqrt(y.re * y.re + y.im * y.im);
-    }
+__device__ __forceinline__ typename OutT<OUT, T>::type out_value(C2<T> y) {
+    if constexpr (OUT == NW_OUT_CWT) return y;
+    else if constexpr (OUT == NW_OUT_POWER) return y.re * y.re + y.im * y.im;
+    else return (T)sqrt(y.re * y.re + y.im * y.im);
 }
 
-// Stockham pass P >= 1: read the LDS image, twiddle, IDFT, write LDS (or HBM if last).
-// Every LDS access is base(thread) + compile-time offset: with the 1-in-32 pad,
-// lds_idx(a + c) = lds_idx(a) + c + c/32 whenever c is a multiple of 32, and for
-// NS < 32 the pad of d0 + r*NS splits into a per-thread and a per-r part.
-template <typename T, int N, int E, int P, int OUT>
-__device__ __forceinline__ void stockham_pass(C2<T>* v, C2<T>* lds, int t, void* orow,
-                                              const C2<T>* __restrict__ tw) {
+// store outputs idx, idx+1 of the current row (orow: wave-uniform row base) as ONE
+// vector store (16 B for complex64, 8 B for float32, 2x16 B for complex128)
+template <int OUT, typename T>
+__device__ __forceinline__ void store_pair(void* orow, uint32_t idx, C2<T> y0, C2<T> y1) {
+    using O = typename OutT<OUT, T>::type;
+    struct alignas(2 * sizeof(O)) P2 { O a, b; };
+#ifdef NW_ABL_NOSTORE
+    asm volatile("" ::"v"(y0.re), "v"(y0.im), "v"(y1.re), "v"(y1.im), "v"(idx));
+    return;
+#endif
+    *at(reinterpret_cast<P2*>(orow), idx * (uint32_t)sizeof(O)) = P2{out_value<OUT, T>(y0), out_value<OUT, T>(y1)};
+}
+template <int OUT, typename T>
+__device__ __forceinline__ void store_one(void* orow, uint32_t idx, C2<T> y) {
+    using O = typename OutT<OUT, T>::type;
+#ifdef NW_ABL_NOSTORE
+    asm volatile("" ::"v"(y.re), "v"(y.im), "v"(idx));
+    return;
+#endif
+    *at(reinterpret_cast<O*>(orow), idx * (uint32_t)sizeof(O)) = out_value<OUT, T>(y);
+}
+
+// two adjacent real slots of the half image, one 8/16-byte LDS access
+template <typename T> struct alignas(2 * sizeof(T)) Pair {
+    T a, b;
+};
+
+template <int COMP, typename T> __device__ __forceinline__ T& comp(C2<T>& c) {
+    if constexpr (COMP == 0) return c.re; else return c.im;
+}
+
+// ---- one component of the pass-P outputs -> LDS (P = 0: slots t*E + s, as pairs)
+template <typename T, int N, int E, int P, int COMP>
+__device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
     using G = Geometry<N, E>;
-    constexpr int R = G::radix(P);
-    constexpr int NS = G::ns(P);
-    constexpr int Q = E / R;             // butterflies per thread
-    constexpr int STRIDE = N / R;        // a multiple of 32 for every supported geometry
-    constexpr bool LAST = (P == G::npass() - 1);
-    static_assert(STRIDE % 32 == 0, "read stride must keep the pad linear");
+    if constexpr (P == 0) {
+        Pair<T>* dst = reinterpret_cast<Pair<T>*>(lds + lds_idx<E>(t * E));
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        const C2<T>* src = lds + lds_idx(t + q * G::T);
+        for (int u = 0; u < E / 2; ++u)
+            dst[u] = Pair<T>{comp<COMP>(v[bitrev<E>(2 * u)]), comp<COMP>(v[bitrev<E>(2 * u + 1)])};
+    } else {
+        constexpr int R = G::radix(P);
+        constexpr int NS = G::ns(P);
+        constexpr int Q = E / R;
 #pragma unroll
-        for (int r = 0; r < R; ++r) v[q * R + r] = src[r * (STRIDE + STRIDE / 32)];
-    }
-    __syncthreads();   // every read of this pass done before the image is overwritten
+        for (int q = 0; q < Q; ++q) {
+            const int j = t + q * G::T;
+            T* dst = lds + lds_idx<E>((j / NS) * NS * R + j % NS);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-        const int j = t + q * G::T;
-        const int m = j % NS;
-        twiddle<T, R, N, NS * R>(v + q * R, m, tw);
-        idft_br<T, R>(v + q * R);
-        const int d0 = (j / NS) * NS * R + m;
-        if constexpr (LAST) {
-            // NS * R == N here, so d0 == j: row-contiguous stores across the wave
-#pragma unroll
-            for (int i = 0; i < R; ++i)
-                store_out<OUT, T>(orow, (uint32_t)(d0 + bitrev<R>(i) * NS), v[q * R + i]);
-        } else {
-            C2<T>* dst;
-            if constexpr (NS % 32 == 0)
-                dst = lds + lds_idx(d0);
-            else
-                dst = lds + d0 + (((j / NS) * NS * R) >> 5);
-#pragma unroll
-            for (int i = 0; i < R; ++i) {
-                const int c = bitrev<R>(i) * NS;
-                dst[(NS % 32 == 0) ? c + c / 32 : c + (c >> 5)] = v[q * R + i];
-            }
+            for (int i = 0; i < R; ++i) dst[lds_off<E>(bitrev<R>(i) * NS)] = comp<COMP>(v[q * R + i]);
         }
     }
-    if constexpr (!LAST) __syncthreads();
 }
 
+// ---- one component of the pass-P inputs <- LDS.  Butterflies: j = t + q*T, except
+// in the LAST pass, where j = Q*t + q so a thread's outputs come in adjacent pairs.
+template <int N, int E, int P> struct PassInfo {
+    using G = Geometry<N, E>;
+    static constexpr int R = G::radix(P);
+    static constexpr int NS = G::ns(P);
+    static constexpr int Q = E / R;
+    static constexpr int STRIDE = N / R;
+    static constexpr bool LAST = (P == G::npass() - 1);
+    static constexpr bool PAIRED = LAST && Q >= 2;
+    static_assert(STRIDE % E == 0 && NS % E == 0, "pad must stay linear");
+    __device__ static __forceinline__ int bfly(int t, int q) { return PAIRED ? Q * t + q : t + q * G::T; }
+};
+
+template <typename T, int N, int E, int P, int COMP>
+__device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
+    using I = PassInfo<N, E, P>;
+    constexpr int R = I::R, Q = I::Q;
+    if constexpr (I::PAIRED) {
+        const T* src = lds + lds_idx<E>(Q * t);
+#pragma unroll
+        for (int q = 0; q < Q; q += 2)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const Pair<T> pr = *reinterpret_cast<const Pair<T>*>(src + q + lds_off<E>(r * I::STRIDE));
+                comp<COMP>(v[q * R + r]) = pr.a;
+                comp<COMP>(v[(q + 1) * R + r]) = pr.b;
+            }
+    } else {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const T* src = lds + lds_idx<E>(t + q * Geometry<N, E>::T);
+#pragma unroll
+            for (int r = 0; r < R; ++r) comp<COMP>(v[q * R + r]) = src[lds_off<E>(r * I::STRIDE)];
+        }
+    }
+}
+
+// ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P
 template <typename T, int N, int E, int OUT, int P>
-__device__ __forceinline__ void run_passes(C2<T>* v, C2<T>* lds, int t, void* orow,
-                                           const C2<T>* __restrict__ tw) {
-    using G = Geometry<N, E>;
-    if constexpr (P < G::npass()) {
-        stockham_pass<T, N, E, P, OUT>(v, lds, t, orow, tw);
-        run_passes<T, N, E, OUT, P + 1>(v, lds, t, orow, tw);
+__device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, void* orow, const C2<T>* __restrict__ tw) {
+    using I = PassInfo<N, E, P>;
+    if constexpr (P < Geometry<N, E>::npass()) {
+        constexpr int R = I::R, Q = I::Q;
+        __syncthreads();                       // earlier readers of the image are done
+        lds_write<T, N, E, P - 1, 0>(v, lds, t);
+        __syncthreads();
+        lds_read<T, N, E, P, 0>(v, lds, t);
+        __syncthreads();
+        lds_write<T, N, E, P - 1, 1>(v, lds, t);
+        __syncthreads();
+        lds_read<T, N, E, P, 1>(v, lds, t);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+#ifndef NW_ABL_NOTWIDDLE
+            twiddle<T, R, N, I::NS * R>(v + q * R, I::bfly(t, q) % I::NS, tw);
+#endif
+            idft_br<T, R>(v + q * R);
+        }
+        if constexpr (I::LAST) {
+            // NS * R == N: the output index of (j, r) is j + r*NS
+#pragma unroll
+            for (int q = 0; q < Q; q += (I::PAIRED ? 2 : 1))
+#pragma unroll
+                for (int i = 0; i < R; ++i) {
+                    const uint32_t k = (uint32_t)(I::bfly(t, q) + bitrev<R>(i) * I::NS);
+                    if constexpr (I::PAIRED)
+                        store_pair<OUT, T>(orow, k, v[q * R + i], v[(q + 1) * R + i]);
+                    else
+                        store_one<OUT, T>(orow, k, v[q * R + i]);
+                }
+        } else {
+            passes_from<T, N, E, OUT, P + 1>(v, lds, t, orow, tw);
+        }
     }
 }
 
-template <typename T, bool REALW> struct WReg;
-template <typename T> struct WReg<T, true> {
-    T re;
-    __device__ __forceinline__ void set(cplx<T> w) { re = w.re; }
-    __device__ __forceinline__ C2<T> apply(cplx<T> x) const { return {re * x.re, re * x.im}; }
+template <typename T, bool REALW> struct WLoad;
+template <typename T> struct WLoad<T, true> {     // analytic wavelets: real rows
+    using type = T;
+    __device__ static __forceinline__ C2<T> apply(T w, C2<T> x) { return {w * x.re, w * x.im}; }
 };
-template <typename T> struct WReg<T, false> {
-    T re, im;
-    __device__ __forceinline__ void set(cplx<T> w) { re = w.re; im = w.im; }
-    __device__ __forceinline__ C2<T> apply(cplx<T> x) const {
-        return {re * x.re - im * x.im, re * x.im + im * x.re};
-    }
+template <typename T> struct WLoad<T, false> {    // table wavelets: complex rows
+    using type = C2<T>;
+    __device__ static __forceinline__ C2<T> apply(C2<T> w, C2<T> x) { return cmul(w, x); }
 };
 
+// Occupancy target (waves per SIMD).  E = 16: 4 (<= 128 VGPRs; the small half images
+// let several blocks share a CU, so one block's barriers and memory waits overlap
+// another's arithmetic).  E = 32 (n = 16384 fp32): one signal occupies 128 KiB of
+// registers, so 2 (<= 256 VGPRs); capping it at 128 spills (measured 1.6x slower).
+#ifndef NW_WAVES_PER_SIMD
+#define NW_WAVES_PER_SIMD(E) ((E) >= 32 ? 2 : 4)
+#endif
 template <typename T, int N, int E, int OUT, bool REALW>
-__global__ __launch_bounds__(N / E) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X, void* __restrict__ out,
-                                                         const C2<T>* __restrict__ tw, int64_t nsig, int group,
-                                                         int nsg_pad) {
+__global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(E)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
+                                                            const void* __restrict__ wtab, void* __restrict__ out,
+                                                            const C2<T>* __restrict__ tw, int64_t nsig, int group,
+                                                            int nsg_pad) {
     using G = Geometry<N, E>;
+    using WT = typename WLoad<T, REALW>::type;
     extern __shared__ __align__(16) unsigned char smem[];
-    C2<T>* lds = reinterpret_cast<C2<T>*>(smem);
+    T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
 
     // XCD-aware block -> (scale, signal group): blocks b, b+8, b+16, ... share an
@@ -268,51 +349,59 @@ __global__ __launch_bounds__(N / E) void nw_fused_kernel(WDesc d, const cplx<T>*
     // fetched from HBM once and re-read from L2 for every scale.
     const int b = blockIdx.x;
     const int xcd = b & 7;
-    const int q = b >> 3;
-    const int fi = q % d.nfreq;
-    const int sg = (q / d.nfreq) * 8 + xcd;
+    const int qb = b >> 3;
+    const int fi = qb % d.nfreq;
+    const int sg = (qb / d.nfreq) * 8 + xcd;
     if (sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
     const int64_t s_begin = (int64_t)sg * group;
     const int64_t s_end = min(nsig, s_begin + group);
-
-    // 1. wavelet bins of this thread, evaluated once per block (1/n folded in)
-    WReg<T, REALW> w[E];
-#pragma unroll
-    for (int r = 0; r < E; ++r) w[r].set(wavelet_bin<T>(d, fi, t + r * G::T));
+    const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * N;   // W[f, :] incl. pad_to and 1/n
 
     for (int64_t s = s_begin; s < s_end; ++s) {
         const C2<T>* xs = reinterpret_cast<const C2<T>*>(X + s * d.nh);
         C2<T> v[E];
-        // 2. pass 0 (Ns = 1): z = W * X at k = t + r*T, radix-E IDFT in registers.
-        //    k < N/2 exactly when r < E/2 (compile-time), so the half-spectrum read
-        //    needs no branch: X[k] directly, or conj(X[N - k]) for the upper half
-        //    (N - k <= N/2 < nh; at k = N/2 the Nyquist bin is real).
+        // pass 0 (Ns = 1): z = W * X at k = t + r*T, radix-E IDFT in registers.
+        // k < N/2 exactly when r < E/2 (compile-time), so the half-spectrum read needs
+        // no branch: X[k], or conj(X[N - k]) above N/2 (at k = N/2 the bin is real).
 #pragma unroll
         for (int r = 0; r < E; ++r) {
+            const uint32_t k = (uint32_t)(t + r * G::T);
             C2<T> x;
+#ifdef NW_ABL_NOXLOAD
+            x = {(T)(t + r), (T)r};
+            asm volatile("" : "+v"(x.re), "+v"(x.im));
+#else
             if (r < E / 2) {
-                x = *at(xs, (uint32_t)(t + r * G::T) * (uint32_t)sizeof(C2<T>));
+                x = *at(xs, k * (uint32_t)sizeof(C2<T>));
             } else {
-                x = *at(xs, (uint32_t)(N - t - r * G::T) * (uint32_t)sizeof(C2<T>));
+                x = *at(xs, ((uint32_t)N - k) * (uint32_t)sizeof(C2<T>));
                 x.im = -x.im;
             }
-            const bool keep = t + r * G::T < d.xlim;     // interpolate_alias mask
+#endif
+            const bool keep = (int64_t)k < d.xlim;     // interpolate_alias mask
             x.re = keep ? x.re : T(0);
             x.im = keep ? x.im : T(0);
-            v[r] = w[r].apply(cplx<T>{x.re, x.im});
+            v[r] = WLoad<T, REALW>::apply(*at(wrow, k * (uint32_t)sizeof(WT)), x);
         }
         idft_br<T, E>(v);
-        {   // E | 32, so (t*E + i) >> 5 == (t*E) >> 5 for i < E
-            C2<T>* dst = lds + t * E + ((t * E) >> 5);
-#pragma unroll
-            for (int i = 0; i < E; ++i) dst[bitrev<E>(i)] = v[i];
-        }
-        __syncthreads();
         const int64_t row = (s * d.nfreq + fi) * (int64_t)N;
         void* orow = (char*)out + row * (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T));
-        run_passes<T, N, E, OUT, 1>(v, lds, t, orow, tw);
-        __syncthreads();   // the last pass's LDS reads finish before the next signal's scatter
+        passes_from<T, N, E, OUT, 1>(v, lds, t, orow, tw);
     }
+}
+
+// W[f, k] for the fused engine: the reference's cached row, pad_to'd to n, 1/n folded
+// in (real rows for analytic kinds, complex for tables).  Built once per plan+wavelet.
+template <typename T, bool REALW>
+__global__ __launch_bounds__(256) void wtable_kernel(WDesc d, void* wtab) {
+    const int fi = blockIdx.y;
+    const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (k >= d.n) return;
+    const cplx<T> w = wavelet_bin<T>(d, fi, k);
+    if constexpr (REALW)
+        reinterpret_cast<T*>(wtab)[(int64_t)fi * d.n + k] = w.re;
+    else
+        reinterpret_cast<C2<T>*>(wtab)[(int64_t)fi * d.n + k] = C2<T>{w.re, w.im};
 }
 
 template <typename T>
@@ -366,9 +455,10 @@ hipError_t twiddles_for(int64_t n, int dtype, void** out) {
 constexpr int kGroup = 8;   // signals per block
 
 template <typename T, int N, int E, bool REALW>
-hipError_t launch_n(const WDesc& d, int out_kind, const void* X, void* out, int64_t nsig, hipStream_t s) {
+hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
+                    hipStream_t s) {
     constexpr int threads = N / E;
-    const size_t lds = (size_t)(N + N / 32) * sizeof(C2<T>);
+    const size_t lds = (size_t)lds_elems<N, E>() * sizeof(T);
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
@@ -379,17 +469,17 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, void* out, int6
     const cplx<T>* Xc = reinterpret_cast<const cplx<T>*>(X);
     const C2<T>* twc_ = reinterpret_cast<const C2<T>*>(tw);
     if (out_kind == NW_OUT_CWT)
-        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, out, twc_, nsig, kGroup, (int)nsg_pad);
+        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad);
     else if (out_kind == NW_OUT_POWER)
-        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, out, twc_, nsig, kGroup, (int)nsg_pad);
+        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad);
     else
-        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, out, twc_, nsig, kGroup, (int)nsg_pad);
+        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad);
     return hipGetLastError();
 }
 
 template <typename T, int N, int E, bool REALW>
 hipError_t prepare_one() {
-    const int lds = (int)((N + N / 32) * sizeof(C2<T>));
+    const int lds = (int)(lds_elems<N, E>() * sizeof(T));
     hipError_t e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e == hipSuccess)
@@ -412,16 +502,20 @@ hipError_t prepare_n() {
 
 }  // namespace
 
-// fp32: 2^10..2^14, fp64: 2^10..2^13 (the padded LDS image is <= 132 KiB)
+#ifndef NW_E16384
+#define NW_E16384 32   // elements per thread at n = 16384 fp32 (512 threads)
+#endif
+
+// power-of-two n from 2^10 to 2^14, fp32 and fp64 (half image <= 144 KiB)
 bool fused_supported(int64_t n, int dtype) {
-    if (n < 1024 || (n & (n - 1))) return false;
-    return dtype == NW_F32 ? n <= 16384 : n <= 8192;
+    if (n < 1024 || n > 16384 || (n & (n - 1))) return false;
+    return dtype == NW_F32 || dtype == NW_F64;
 }
 
-#define NW_FUSED_TABLE(X)                                                           \
-    X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, 16) X(float, 8192, 16)    \
-    X(float, 16384, 32) X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) \
-    X(double, 8192, 16)
+#define NW_FUSED_TABLE(X)                                                               \
+    X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, 16) X(float, 8192, 16)        \
+    X(float, 16384, NW_E16384) X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) \
+    X(double, 8192, 16) X(double, 16384, 16)
 
 hipError_t fused_prepare(int64_t n, int dtype) {
 #define NW_PREP(TY, NN, EE) \
@@ -431,13 +525,31 @@ hipError_t fused_prepare(int64_t n, int dtype) {
     return hipErrorNotSupported;
 }
 
-hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, void* out, int64_t nsig,
-                        hipStream_t s) {
+size_t fused_wtable_bytes(int64_t n, int nfreq, int dtype, int kind) {
+    const size_t esz = dtype == NW_F32 ? sizeof(float) : sizeof(double);
+    return (size_t)n * nfreq * esz * (kind == NW_TABLE ? 2 : 1);
+}
+
+hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
+    dim3 grid((unsigned)((d.n + 255) / 256), (unsigned)d.nfreq);
     const bool realw = d.kind != NW_TABLE;
-#define NW_LAUNCH(TY, NN, EE)                                                           \
-    if (d.n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64))                      \
-        return realw ? launch_n<TY, NN, EE, true>(d, out_kind, X, out, nsig, s)         \
-                     : launch_n<TY, NN, EE, false>(d, out_kind, X, out, nsig, s);
+    if (dtype == NW_F32) {
+        if (realw) wtable_kernel<float, true><<<grid, 256, 0, s>>>(d, wtab);
+        else wtable_kernel<float, false><<<grid, 256, 0, s>>>(d, wtab);
+    } else {
+        if (realw) wtable_kernel<double, true><<<grid, 256, 0, s>>>(d, wtab);
+        else wtable_kernel<double, false><<<grid, 256, 0, s>>>(d, wtab);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
+                        int64_t nsig, hipStream_t s) {
+    const bool realw = d.kind != NW_TABLE;
+#define NW_LAUNCH(TY, NN, EE)                                                                 \
+    if (d.n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64))                            \
+        return realw ? launch_n<TY, NN, EE, true>(d, out_kind, X, wtab, out, nsig, s)         \
+                     : launch_n<TY, NN, EE, false>(d, out_kind, X, wtab, out, nsig, s);
     NW_FUSED_TABLE(NW_LAUNCH)
 #undef NW_LAUNCH
     return hipErrorNotSupported;

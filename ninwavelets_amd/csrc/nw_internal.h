@@ -126,8 +126,10 @@ hipError_t launch_epilogue(int dtype, int out_kind, const void* Y, void* out, in
 hipError_t launch_rows(const WDesc& d, int dtype, void* rows, hipStream_t s);
 // fused engine (nw_fused.hip)
 bool       fused_supported(int64_t n, int dtype);
-hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, void* out,
-                        int64_t nsig, hipStream_t s);
 hipError_t fused_prepare(int64_t n, int dtype);
+size_t     fused_wtable_bytes(int64_t n, int nfreq, int dtype, int kind);
+hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s);
+hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
+                        int64_t nsig, hipStream_t s);
 
 }  // namespace nw
