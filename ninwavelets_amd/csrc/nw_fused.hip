@@ -40,15 +40,20 @@ template <typename T> __device__ __forceinline__ C2<T> cmul(C2<T> a, C2<T> b) {
 // the compiler cannot re-associate constant parts back into 64-bit address math.
 // (The raw_buffer_load/store_b64 builtins of this toolchain emit a single dword
 // and are not used.)
+//
+// `lane_off` is a per-thread byte offset shared by many accesses and `c` a
+// compile-time byte offset.  The volatile asm re-materialises lane_off at every
+// use, so neither it nor lane_off + c can be hoisted out of the signal loop as a
+// per-element loop invariant (which left ~100 live offsets and spilled).
 template <typename P>
-__device__ __forceinline__ P* at(P* base, uint32_t byte_off) {
-    asm("" : "+v"(byte_off));
-    return reinterpret_cast<P*>(reinterpret_cast<char*>(base) + byte_off);
+__device__ __forceinline__ P* at(P* base, uint32_t lane_off, uint32_t c = 0) {
+    asm volatile("" : "+v"(lane_off));
+    return reinterpret_cast<P*>(reinterpret_cast<char*>(base) + (lane_off + c));
 }
 template <typename P>
-__device__ __forceinline__ const P* at(const P* base, uint32_t byte_off) {
-    asm("" : "+v"(byte_off));
-    return reinterpret_cast<const P*>(reinterpret_cast<const char*>(base) + byte_off);
+__device__ __forceinline__ const P* at(const P* base, uint32_t lane_off, uint32_t c = 0) {
+    asm volatile("" : "+v"(lane_off));
+    return reinterpret_cast<const P*>(reinterpret_cast<const char*>(base) + (lane_off + c));
 }
 
 // cos(2*pi*i/32), i = 0..31
@@ -125,21 +130,24 @@ template <int R> constexpr int ilog2() { return R <= 1 ? 0 : 1 + ilog2<R / 2>();
 // v[r] *= w^(r m), w = exp(2 pi i / NSR), r = 1..R-1.  The base powers w^(m 2^k)
 // come from the exact table tw[i] = exp(2 pi i i / N) (L2-resident); every other
 // power is a product of at most log2(R) of them: a few ulp, no recurrence drift.
+// The bases are loaded a phase ahead of use (before the LDS exchange that feeds
+// the pass) so the table latency hides under the exchange.
 template <typename T, int R, int N, int NSR>
-__device__ __forceinline__ void twiddle(C2<T>* v, int m, const C2<T>* __restrict__ tw) {
-    if constexpr (R > 1) {
-        constexpr int LR = ilog2<R>();
-        C2<T> p[LR];
+__device__ __forceinline__ void twiddle_bases(C2<T>* p, int m, const C2<T>* __restrict__ tw) {
 #pragma unroll
-        for (int k = 0; k < LR; ++k) p[k] = *at(tw, (uint32_t)((m << k) * (N / NSR) * sizeof(C2<T>)));
+    for (int k = 0; k < ilog2<R>(); ++k)
+        p[k] = *at(tw, (uint32_t)m * (uint32_t)((N / NSR) * sizeof(C2<T>)) << k);
+}
+template <typename T, int R>
+__device__ __forceinline__ void twiddle_apply(C2<T>* v, const C2<T>* p) {
+    constexpr int LR = ilog2<R>();
 #pragma unroll
-        for (int r = 1; r < R; ++r) {
-            C2<T> w = p[__builtin_ctz(r)];
+    for (int r = 1; r < R; ++r) {
+        C2<T> w = p[__builtin_ctz(r)];
 #pragma unroll
-            for (int k = __builtin_ctz(r) + 1; k < LR; ++k)
-                if (r & (1 << k)) w = cmul(w, p[k]);
-            v[r] = cmul(v[r], w);
-        }
+        for (int k = __builtin_ctz(r) + 1; k < LR; ++k)
+            if (r & (1 << k)) w = cmul(w, p[k]);
+        v[r] = cmul(v[r], w);
     }
 }
 
@@ -187,25 +195,67 @@ __device__ __forceinline__ typename OutT<OUT, T>::type out_value(C2<T> y) {
 
 // store outputs idx, idx+1 of the current row (orow: wave-uniform row base) as ONE
 // vector store (16 B for complex64, 8 B for float32, 2x16 B for complex128)
+// outputs lane_idx + c_idx (pair: and the next one) of the current row
 template <int OUT, typename T>
-__device__ __forceinline__ void store_pair(void* orow, uint32_t idx, C2<T> y0, C2<T> y1) {
+__device__ __forceinline__ void store_pair(void* orow, uint32_t lane_idx, uint32_t c_idx, C2<T> y0, C2<T> y1) {
     using O = typename OutT<OUT, T>::type;
     struct alignas(2 * sizeof(O)) P2 { O a, b; };
 #ifdef NW_ABL_NOSTORE
-    asm volatile("" ::"v"(y0.re), "v"(y0.im), "v"(y1.re), "v"(y1.im), "v"(idx));
+    asm volatile("" ::"v"(y0.re), "v"(y0.im), "v"(y1.re), "v"(y1.im), "v"(lane_idx));
     return;
 #endif
-    *at(reinterpret_cast<P2*>(orow), idx * (uint32_t)sizeof(O)) = P2{out_value<OUT, T>(y0), out_value<OUT, T>(y1)};
+#ifndef NW_PLAIN_STORE   // streaming (nt) stores: measured 5 % faster than plain at n = 16384
+    using V = typename std::conditional<sizeof(P2) == 16, float __attribute__((ext_vector_type(4))),
+              typename std::conditional<sizeof(P2) == 8, float __attribute__((ext_vector_type(2))),
+                                        double __attribute__((ext_vector_type(4)))>::type>::type;
+    const P2 pv{out_value<OUT, T>(y0), out_value<OUT, T>(y1)};
+    __builtin_nontemporal_store(__builtin_bit_cast(V, pv),
+                                reinterpret_cast<V*>(at(reinterpret_cast<P2*>(orow), lane_idx * (uint32_t)sizeof(O),
+                                                        c_idx * (uint32_t)sizeof(O))));
+#else
+    *at(reinterpret_cast<P2*>(orow), lane_idx * (uint32_t)sizeof(O), c_idx * (uint32_t)sizeof(O)) =
+        P2{out_value<OUT, T>(y0), out_value<OUT, T>(y1)};
+#endif
 }
 template <int OUT, typename T>
-__device__ __forceinline__ void store_one(void* orow, uint32_t idx, C2<T> y) {
+__device__ __forceinline__ void store_one(void* orow, uint32_t lane_idx, uint32_t c_idx, C2<T> y) {
     using O = typename OutT<OUT, T>::type;
 #ifdef NW_ABL_NOSTORE
-    asm volatile("" ::"v"(y.re), "v"(y.im), "v"(idx));
+    asm volatile("" ::"v"(y.re), "v"(y.im), "v"(lane_idx));
     return;
 #endif
-    *at(reinterpret_cast<O*>(orow), idx * (uint32_t)sizeof(O)) = out_value<OUT, T>(y);
+    *at(reinterpret_cast<O*>(orow), lane_idx * (uint32_t)sizeof(O), c_idx * (uint32_t)sizeof(O)) =
+        out_value<OUT, T>(y);
 }
+
+// ---- diagnostic phase stamps (NW_STAMPS builds only; never in the product build).
+// Per wave: cycles between consecutive stamps are summed into SGPR-resident
+// counters and lane 0 adds them to g_nw_stamps at the end (cdna_hip_programming.md
+// §7 "In-kernel stamps"): read the SHARES, not the run time of a stamped build.
+#ifdef NW_STAMPS
+constexpr int kStamps = 8;
+__device__ unsigned long long g_nw_stamps[kStamps + 1];
+struct Stamps {
+    unsigned long long last, acc[kStamps];
+};
+__device__ __forceinline__ unsigned long long nw_now() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define NW_STAMP(st, k)                                 \
+    do {                                                \
+        const unsigned long long now_ = nw_now();       \
+        (st)->acc[k] += now_ - (st)->last;              \
+        (st)->last = now_;                              \
+    } while (0)
+constexpr int kStampsStore = kStamps - 1;
+#else
+struct Stamps {};
+#define NW_STAMP(st, k) ((void)(st))
+#endif
 
 // two adjacent real slots of the half image, one 8/16-byte LDS access
 template <typename T> struct alignas(2 * sizeof(T)) Pair {
@@ -277,12 +327,65 @@ __device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
     }
 }
 
-// ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P
+// ---- the last pass's outputs: store number i (0 .. nstores-1) of a thread
+template <typename T, int N, int E, int OUT>
+struct LastStores {
+    using I = PassInfo<N, E, Geometry<N, E>::npass() - 1>;
+    static constexpr int R = I::R, Q = I::Q;
+    static constexpr int STEP = I::PAIRED ? 2 : 1;
+    static constexpr int COUNT = Q / STEP * R;      // store instructions per thread per signal
+    template <int K>
+    __device__ static __forceinline__ void one(const C2<T>* o, void* orow, int t) {
+        constexpr int q = (K / R) * STEP, i = K % R;
+        const uint32_t lane = (uint32_t)I::bfly(t, 0);        // Q*t (paired) or t
+        constexpr uint32_t c = (uint32_t)((I::PAIRED ? q : q * Geometry<N, E>::T) + bitrev<R>(i) * I::NS);
+        if constexpr (I::PAIRED)
+            store_pair<OUT, T>(orow, lane, c, o[q * R + i], o[(q + 1) * R + i]);
+        else
+            store_one<OUT, T>(orow, lane, c, o[q * R + i]);
+    }
+    // stores [C*COUNT/NCH, (C+1)*COUNT/NCH) -- one chunk of a deferred signal
+    template <int C, int NCH, int K = C * COUNT / NCH>
+    __device__ static __forceinline__ void chunk(const C2<T>* o, void* orow, int t) {
+        if constexpr (K < (C + 1) * COUNT / NCH) {
+            one<K>(o, orow, t);
+            chunk<C, NCH, K + 1>(o, orow, t);
+        }
+    }
+};
+
+// Store chunks of the PREVIOUS signal are interleaved with this signal's phases
+// (kChunks points: after pass 0, then around every exchange), so the CU's store
+// queue drains continuously instead of in one burst that stalls every wave.
+constexpr int kChunks = 4;
+
+#ifndef NW_DEFER
+#define NW_DEFER 0     // deferred/interleaved stores: measured no gain (the CU store path is the limit)
+#endif
+
+template <typename T, int N, int E, int OUT, int C>
+__device__ __forceinline__ void drain(const C2<T>* o, void* oprev, int t) {
+    if constexpr (NW_DEFER && C < kChunks)
+        if (oprev) LastStores<T, N, E, OUT>::template chunk<C, kChunks>(o, oprev, t);
+}
+
+// ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P.
+// In the last pass the NEXT signal's X is loaded (into x) before anything else is
+// issued: loads and stores retire in one in-order vmcnt queue, so the next pass 0
+// waits for its loads only.  The outputs are moved to o and stored during the
+// next signal (drain) or by the caller after the last signal.
 template <typename T, int N, int E, int OUT, int P>
-__device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, void* orow, const C2<T>* __restrict__ tw) {
+__device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>* __restrict__ tw, C2<T>* x,
+                                            const C2<T>* xs_next, bool interp, C2<T>* o, void* oprev, void* ocur,
+                                            Stamps* st) {
     using I = PassInfo<N, E, P>;
     if constexpr (P < Geometry<N, E>::npass()) {
-        constexpr int R = I::R, Q = I::Q;
+        constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
+        C2<T> pb[Q][LR > 0 ? LR : 1];
+#ifndef NW_ABL_NOTWIDDLE
+#pragma unroll
+        for (int q = 0; q < Q; ++q) twiddle_bases<T, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
+#endif
         __syncthreads();                       // earlier readers of the image are done
         lds_write<T, N, E, P - 1, 0>(v, lds, t);
         __syncthreads();
@@ -291,28 +394,58 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, void* orow,
         lds_write<T, N, E, P - 1, 1>(v, lds, t);
         __syncthreads();
         lds_read<T, N, E, P, 1>(v, lds, t);
+        drain<T, N, E, OUT, 2 * P - 1>(o, oprev, t);
+        NW_STAMP(st, 2 * P - 1);               // exchange P-1 -> P
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
 #ifndef NW_ABL_NOTWIDDLE
-            twiddle<T, R, N, I::NS * R>(v + q * R, I::bfly(t, q) % I::NS, tw);
+            twiddle_apply<T, R>(v + q * R, pb[q]);
 #endif
             idft_br<T, R>(v + q * R);
         }
+        NW_STAMP(st, 2 * P);                   // pass P arithmetic
         if constexpr (I::LAST) {
-            // NS * R == N: the output index of (j, r) is j + r*NS
+            drain<T, N, E, OUT, 2 * P>(o, oprev, t);        // anything left of the previous signal
+            if constexpr (2 * P < kChunks - 1) {
+                drain<T, N, E, OUT, 2 * P + 1>(o, oprev, t);
+                drain<T, N, E, OUT, 2 * P + 2>(o, oprev, t);
+            }
+            if (xs_next) load_x<T, N, E>(x, xs_next, t, interp);
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (NW_DEFER) {
 #pragma unroll
-            for (int q = 0; q < Q; q += (I::PAIRED ? 2 : 1))
-#pragma unroll
-                for (int i = 0; i < R; ++i) {
-                    const uint32_t k = (uint32_t)(I::bfly(t, q) + bitrev<R>(i) * I::NS);
-                    if constexpr (I::PAIRED)
-                        store_pair<OUT, T>(orow, k, v[q * R + i], v[(q + 1) * R + i]);
-                    else
-                        store_one<OUT, T>(orow, k, v[q * R + i]);
-                }
+                for (int k = 0; k < E; ++k) o[k] = v[k];
+            } else {
+                LastStores<T, N, E, OUT>::template chunk<0, 1>(v, ocur, t);
+            }
         } else {
-            passes_from<T, N, E, OUT, P + 1>(v, lds, t, orow, tw);
+            drain<T, N, E, OUT, 2 * P>(o, oprev, t);
+            passes_from<T, N, E, OUT, P + 1>(v, lds, t, tw, x, xs_next, interp, o, oprev, ocur, st);
         }
+    }
+}
+
+// X[k] at the thread's pass-0 bins k = t + r*T from the R2C half spectrum xs.
+// k < N/2 exactly when r < E/2 (compile-time), so no branch: X[k], or conj(X[N - k])
+// above N/2 (at k = N/2 the bin is real).  interpolate_alias zeroes k >= int(N/2).
+template <typename T, int N, int E>
+__device__ __forceinline__ void load_x(C2<T>* x, const C2<T>* xs, int t, bool interp) {
+    constexpr int TT = N / E;
+    const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(C2<T>);
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+#ifdef NW_ABL_NOXLOAD
+        x[r] = {(T)(t + r), (T)r};
+        asm volatile("" : "+v"(x[r].re), "+v"(x[r].im));
+#else
+        if (r < E / 2) {
+            x[r] = *at(xs, xo, (uint32_t)(r * TT * sizeof(C2<T>)));
+        } else {   // X[N - k] = X[(N - r*T) - t]
+            x[r] = *at(xs, (uint32_t)((N - r * TT) * sizeof(C2<T>)) - xo);
+            x[r].im = -x[r].im;
+        }
+#endif
+        if (r >= E / 2 && interp) x[r] = C2<T>{T(0), T(0)};
     }
 }
 
@@ -326,15 +459,23 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
     __device__ static __forceinline__ C2<T> apply(C2<T> w, C2<T> x) { return cmul(w, x); }
 };
 
-// Occupancy target (waves per SIMD).  E = 16: 4 (<= 128 VGPRs; the small half images
-// let several blocks share a CU, so one block's barriers and memory waits overlap
-// another's arithmetic).  E = 32 (n = 16384 fp32): one signal occupies 128 KiB of
-// registers, so 2 (<= 256 VGPRs); capping it at 128 spills (measured 1.6x slower).
-#ifndef NW_WAVES_PER_SIMD
-#define NW_WAVES_PER_SIMD(E) ((E) >= 32 ? 2 : 4)
+// Occupancy target: 4 waves per SIMD (<= 128 VGPRs).  The half image is <= 74 KiB
+// (fp32), so two 512-thread blocks share a CU at n = 16384 (more at smaller n) and
+// one block's barriers, memory waits and store bursts overlap another's arithmetic.
+constexpr int kGroup = 4;   // signals per block
+constexpr int kTileF = 8;   // scales per XCD tile
+constexpr int kTileG = 8;   // signal groups per XCD tile
+
+#ifndef NW_WPS32
+#define NW_WPS32 2
 #endif
+#ifndef NW_WPS16
+#define NW_WPS16 4
+#endif
+// fp64 holds twice the registers per element: 2 waves per SIMD
+#define NW_WAVES_PER_SIMD(T, E) (sizeof(T) == 8 || (E) >= 32 ? NW_WPS32 : NW_WPS16)
 template <typename T, int N, int E, int OUT, bool REALW>
-__global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(E)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
+__global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
                                                             const void* __restrict__ wtab, void* __restrict__ out,
                                                             const C2<T>* __restrict__ tw, int64_t nsig, int group,
                                                             int nsg_pad) {
@@ -344,50 +485,67 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(E)) void nw_fused_kernel(W
     T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
 
-    // XCD-aware block -> (scale, signal group): blocks b, b+8, b+16, ... share an
-    // XCD (and its L2) and walk the scales of ONE signal group, so X[s] is
-    // fetched from HBM once and re-read from L2 for every scale.
+    // XCD-aware block -> (scale, signal group).  Blocks b, b+8, b+16, ... share an XCD
+    // (and its 4 MiB L2); the ~64 of them resident at a time cover a tile of
+    // kTileF scales x kTileG signal groups, so each W row is read by kTileG blocks
+    // and each X group by kTileF blocks from L2 (W + X of a tile ~2.5 MiB), and
+    // the XCD sweeps all scales of its groups before moving on.
     const int b = blockIdx.x;
     const int xcd = b & 7;
-    const int qb = b >> 3;
-    const int fi = qb % d.nfreq;
-    const int sg = (qb / d.nfreq) * 8 + xcd;
-    if (sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
+    const int local = b >> 3;
+    const int pos = local % (kTileF * kTileG);
+    const int round = local / (kTileF * kTileG);
+    const int nfr = (d.nfreq + kTileF - 1) / kTileF;
+    const int fi = (round % nfr) * kTileF + pos % kTileF;
+    const int sg = ((round / nfr) * kTileG + pos / kTileF) * 8 + xcd;
+    if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
     const int64_t s_begin = (int64_t)sg * group;
     const int64_t s_end = min(nsig, s_begin + group);
-    const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * N;   // W[f, :] incl. pad_to and 1/n
+    // interpolate_alias zeroes X[k], k >= int(N/2); k = t + r*T >= N/2 exactly when r >= E/2
+    const bool interp = d.xlim < N;
 
-    for (int64_t s = s_begin; s < s_end; ++s) {
-        const C2<T>* xs = reinterpret_cast<const C2<T>*>(X + s * d.nh);
-        C2<T> v[E];
-        // pass 0 (Ns = 1): z = W * X at k = t + r*T, radix-E IDFT in registers.
-        // k < N/2 exactly when r < E/2 (compile-time), so the half-spectrum read needs
-        // no branch: X[k], or conj(X[N - k]) above N/2 (at k = N/2 the bin is real).
+    // W[f, k] at the thread's bins, evaluated once per block into registers (1/n folded in)
+    WT w[E];
 #pragma unroll
-        for (int r = 0; r < E; ++r) {
-            const uint32_t k = (uint32_t)(t + r * G::T);
-            C2<T> x;
-#ifdef NW_ABL_NOXLOAD
-            x = {(T)(t + r), (T)r};
-            asm volatile("" : "+v"(x.re), "+v"(x.im));
-#else
-            if (r < E / 2) {
-                x = *at(xs, k * (uint32_t)sizeof(C2<T>));
-            } else {
-                x = *at(xs, ((uint32_t)N - k) * (uint32_t)sizeof(C2<T>));
-                x.im = -x.im;
-            }
-#endif
-            const bool keep = (int64_t)k < d.xlim;     // interpolate_alias mask
-            x.re = keep ? x.re : T(0);
-            x.im = keep ? x.im : T(0);
-            v[r] = WLoad<T, REALW>::apply(*at(wrow, k * (uint32_t)sizeof(WT)), x);
-        }
-        idft_br<T, E>(v);
-        const int64_t row = (s * d.nfreq + fi) * (int64_t)N;
-        void* orow = (char*)out + row * (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T));
-        passes_from<T, N, E, OUT, 1>(v, lds, t, orow, tw);
+    for (int r = 0; r < E; ++r) {
+        const cplx<T> wb = wavelet_bin<T>(d, fi, t + r * G::T);
+        if constexpr (REALW) w[r] = wb.re; else w[r] = C2<T>{wb.re, wb.im};
     }
+
+#ifdef NW_STAMPS
+    Stamps stamps{};
+    Stamps* st = &stamps;
+    st->last = nw_now();
+#else
+    Stamps* st = nullptr;
+#endif
+    C2<T> x[E];
+    C2<T> o[E];                    // outputs of the previous signal, stored during this one
+    void* oprev = nullptr;
+    const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T));
+    load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s_begin * d.nh), t, interp);
+    for (int64_t s = s_begin; s < s_end; ++s) {
+        // pass 0 (Ns = 1): z = W * X at k = t + r*T, radix-E IDFT in registers
+        C2<T> v[E];
+#pragma unroll
+        for (int r = 0; r < E; ++r) v[r] = WLoad<T, REALW>::apply(w[r], x[r]);
+        idft_br<T, E>(v);
+        drain<T, N, E, OUT, 0>(o, oprev, t);
+        NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
+        const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
+        void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
+        passes_from<T, N, E, OUT, 1>(v, lds, t, tw, x, xs_next, interp, o, oprev, ocur, st);
+        oprev = ocur;
+    }
+    // the last signal's outputs
+    if constexpr (NW_DEFER) LastStores<T, N, E, OUT>::template chunk<0, 1>(o, oprev, t);
+    NW_STAMP(st, kStampsStore);
+#ifdef NW_STAMPS
+    if ((t & 63) == 0) {
+        for (int k = 0; k < kStamps; ++k) atomicAdd(&g_nw_stamps[k], stamps.acc[k]);
+        atomicAdd(&g_nw_stamps[kStamps], (unsigned long long)(s_end - s_begin));
+    }
+#endif
 }
 
 // W[f, k] for the fused engine: the reference's cached row, pad_to'd to n, 1/n folded
@@ -452,7 +610,6 @@ hipError_t twiddles_for(int64_t n, int dtype, void** out) {
     return hipSuccess;
 }
 
-constexpr int kGroup = 8;   // signals per block
 
 template <typename T, int N, int E, bool REALW>
 hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
@@ -463,8 +620,9 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
     const int64_t nsg = (nsig + kGroup - 1) / kGroup;
-    const int64_t nsg_pad = (nsg + 7) / 8 * 8;
-    const int64_t blocks = nsg_pad * d.nfreq;
+    const int64_t nsg_pad = (nsg + 8 * kTileG - 1) / (8 * kTileG) * (8 * kTileG);
+    const int64_t nfr = (d.nfreq + kTileF - 1) / kTileF;
+    const int64_t blocks = nsg_pad * nfr * kTileF;
     if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
     const cplx<T>* Xc = reinterpret_cast<const cplx<T>*>(X);
     const C2<T>* twc_ = reinterpret_cast<const C2<T>*>(tw);
@@ -506,16 +664,17 @@ hipError_t prepare_n() {
 #define NW_E16384 32   // elements per thread at n = 16384 fp32 (512 threads)
 #endif
 
-// power-of-two n from 2^10 to 2^14, fp32 and fp64 (half image <= 144 KiB)
+// power-of-two n: 2^10..2^14 in fp32, 2^10..2^13 in fp64 (registers: one fp64
+// signal of 16384 points does not fit a 512-thread block's VGPR budget)
 bool fused_supported(int64_t n, int dtype) {
-    if (n < 1024 || n > 16384 || (n & (n - 1))) return false;
-    return dtype == NW_F32 || dtype == NW_F64;
+    if (n < 1024 || (n & (n - 1))) return false;
+    return dtype == NW_F32 ? n <= 16384 : (dtype == NW_F64 && n <= 8192);
 }
 
 #define NW_FUSED_TABLE(X)                                                               \
     X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, 16) X(float, 8192, 16)        \
     X(float, 16384, NW_E16384) X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) \
-    X(double, 8192, 16) X(double, 16384, 16)
+    X(double, 8192, 16)
 
 hipError_t fused_prepare(int64_t n, int dtype) {
 #define NW_PREP(TY, NN, EE) \
@@ -556,3 +715,16 @@ hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, 
 }
 
 }  // namespace nw
+
+#ifdef NW_STAMPS
+// diagnostic builds only: per-phase cycle sums (and the signal-wave count in [8])
+extern "C" int nw_debug_stamps(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nw::g_nw_stamps), sizeof(unsigned long long) * 9) != hipSuccess)
+        return -2;
+    if (reset) {
+        unsigned long long z[9] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(nw::g_nw_stamps), z, sizeof(z)) != hipSuccess) return -2;
+    }
+    return 0;
+}
+#endif
