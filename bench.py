@@ -59,6 +59,20 @@ def synth_device(torch, S, n, seed, device, sfreq=1000.):
     return x
 
 
+def pmc_traffic(kernel, config, chunk, engine):
+    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
+    same bench command (tools/gpu_round.sh -> profiles/pmc_<config>_<engine>.json), or None."""
+    path = os.path.join(ROOT, 'profiles', f'pmc_{config}_{engine}.json')
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get('kernel') != kernel or d.get('config', {}).get('chunk') != chunk:
+        return None
+    return d.get('hbm_bytes_per_launch')
+
+
 def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0):
     """The CPU oracle (numpy + scipy.fftpack, the reference's arithmetic) on one core,
     W built once (reuse=True) and excluded, timed over as many signals as fit the budget."""
@@ -167,9 +181,11 @@ def main():
             out_e = 2 * esz                    # K1 always writes the complex product
         per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
         achieved = per_launch / (ms * 1e-3) / 1e9
-        roof = {'kernel': 'nw_fused' if fused else 'k1_multiply', 'bound': 'hbm',
+        kname = 'nw_fused' if fused else 'k1_multiply'
+        roof = {'kernel': kname, 'bound': 'hbm',
                 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
-                'frac': round(achieved / PEAK_HBM_GBPS, 4), 'traffic': None,
+                'frac': round(achieved / PEAK_HBM_GBPS, 4),
+                'traffic': pmc_traffic(kname, args.config, C, st['engine']),
                 'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
         stage_ms = {k: round(st[k] / args.steps, 3) for k in
                     ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_copy')}
