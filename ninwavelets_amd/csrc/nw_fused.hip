@@ -22,6 +22,15 @@
 
 #include "nw_internal.h"
 
+#ifndef NW_HWTWIDDLE
+#define NW_HWTWIDDLE 1   // fp32 twiddles from v_cos/v_sin (no loads); fp64 always uses the table
+#endif
+#ifndef NW_XDMA_MIN_E
+#define NW_XDMA_MIN_E 32 // fp32 with E >= this: the next signal's X copied into the idle LDS
+                         // image by LDS-DMA before the stores (measured: E=32 1.99 -> 1.94 ms,
+                         // E=16 0.362 -> 0.386 ms, so off there)
+#endif
+
 namespace nw {
 
 namespace {
@@ -134,9 +143,21 @@ template <int R> constexpr int ilog2() { return R <= 1 ? 0 : 1 + ilog2<R / 2>();
 // the pass) so the table latency hides under the exchange.
 template <typename T, int R, int N, int NSR>
 __device__ __forceinline__ void twiddle_bases(C2<T>* p, int m, const C2<T>* __restrict__ tw) {
+    // the twiddles depend on the thread only: keep the compiler from hoisting all of
+    // them out of the signal loop (that keeps ~120 values live and spills)
+    asm volatile("" : "+v"(m));
 #pragma unroll
-    for (int k = 0; k < ilog2<R>(); ++k)
-        p[k] = *at(tw, (uint32_t)m * (uint32_t)((N / NSR) * sizeof(C2<T>)) << k);
+    for (int k = 0; k < ilog2<R>(); ++k) {
+        if constexpr (sizeof(T) == 4 && NW_HWTWIDDLE) {
+            // v_cos/v_sin take revolutions; (m << k) / NSR is exact in fp32 (power-of-two
+            // denominator), measured max abs error 1.2e-7 over all 16384 angles: no memory
+            // access, so nothing queues behind this wave's in-flight stores
+            const float rev = (float)(m << k) * (1.0f / (float)NSR);
+            p[k] = C2<T>{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
+        } else {
+            p[k] = *at(tw, (uint32_t)m * (uint32_t)((N / NSR) * sizeof(C2<T>)) << k);
+        }
+    }
 }
 template <typename T, int R>
 __device__ __forceinline__ void twiddle_apply(C2<T>* v, const C2<T>* p) {
@@ -327,6 +348,52 @@ __device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
     }
 }
 
+// Workgroup barrier for the LDS image only.  __syncthreads() carries a workgroup
+// release fence that gfx950 lowers to s_waitcnt vmcnt(0): every exchange would
+// wait for ALL of the wave's in-flight global stores.  The exchanges only need
+// this wave's LDS operations complete (lgkmcnt(0)) before the s_barrier.
+__device__ __forceinline__ void lds_barrier() {
+#ifdef NW_FENCED_BARRIER
+    __syncthreads();
+#else
+    __builtin_amdgcn_s_waitcnt(0xC07F);   // vmcnt(63) expcnt(7) lgkmcnt(0): LDS ops only
+    __builtin_amdgcn_s_barrier();
+#endif
+}
+
+// ---- LDS-DMA of the next signal's half spectrum X[0 .. N/2) (N*4 bytes) into the idle
+// LDS image: 16 B per lane per instruction, global_load_lds_dwordx4 writes lane l of
+// a wave at (wave-uniform base) + 16*l.  X[N/2] (the real Nyquist bin) travels by a
+// scalar load.  The DMA is issued before the stores, so the next pass 0 waits for
+// it with vmcnt(#stores issued after it), not for the stores.
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef __attribute__((address_space(1))) void gbl_void_t;
+
+template <int N, int TT>
+__device__ __forceinline__ void dma_x(const C2<float>* xs, float* lds, int t) {
+    constexpr int CH = N * 4 / 16;                 // 16-byte chunks of X[0 .. N/2)
+    static_assert(CH % TT == 0, "whole DMA rounds");
+    const int wave_base = (t & ~63) * 16;
+    const uint32_t lane_off = (uint32_t)t * 16u;
+#pragma unroll
+    for (int i = 0; i < CH / TT; ++i) {
+        // uniform chunk base + opaque 32-bit lane offset: the saddr form, no 64-bit VGPR pairs
+        const char* chunk = reinterpret_cast<const char*>(xs) + (size_t)i * TT * 16;
+        asm volatile("" : "+s"(chunk));           // computed here, in SGPRs (not hoisted)
+        const char* src = at(chunk, lane_off);
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
+                                         (lds_void_t*)(reinterpret_cast<char*>(lds) + i * TT * 16 + wave_base), 16,
+                                         0, 0);
+    }
+}
+
+// s_waitcnt vmcnt(V) with expcnt/lgkmcnt left free (gfx9 encoding: vmcnt[3:0] + [15:14])
+template <int V>
+__device__ __forceinline__ void wait_vmcnt() {
+    static_assert(V >= 0 && V < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((V & 0xF) | ((V >> 4) << 14) | 0x70 | 0xF00);
+}
+
 // ---- the last pass's outputs: store number i (0 .. nstores-1) of a thread
 template <typename T, int N, int E, int OUT>
 struct LastStores {
@@ -359,9 +426,19 @@ struct LastStores {
 // queue drains continuously instead of in one burst that stalls every wave.
 constexpr int kChunks = 4;
 
+#ifndef NW_WMODE
+#define NW_WMODE 1      // 0: W in registers for the block; 1: W loaded in pass 0; 2: re-evaluated
+#endif
+#ifndef NW_XPREFETCH
+#define NW_XPREFETCH 0   // 1: next signal's X loaded into registers ahead of the stores (needs the
+                         // 256-VGPR budget; with 2 blocks per CU the other block hides the wait)
+#endif
 #ifndef NW_DEFER
 #define NW_DEFER 0     // deferred/interleaved stores: measured no gain (the CU store path is the limit)
 #endif
+
+// complex W rows (tables) keep the register path: with LDS-DMA they exceed 128 VGPRs
+template <typename T, int E, bool REALW> constexpr bool kXDMA = sizeof(T) == 4 && E >= NW_XDMA_MIN_E && REALW;
 
 template <typename T, int N, int E, int OUT, int C>
 __device__ __forceinline__ void drain(const C2<T>* o, void* oprev, int t) {
@@ -374,7 +451,7 @@ __device__ __forceinline__ void drain(const C2<T>* o, void* oprev, int t) {
 // issued: loads and stores retire in one in-order vmcnt queue, so the next pass 0
 // waits for its loads only.  The outputs are moved to o and stored during the
 // next signal (drain) or by the caller after the last signal.
-template <typename T, int N, int E, int OUT, int P>
+template <typename T, int N, int E, int OUT, int P, bool XD>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, bool interp, C2<T>* o, void* oprev, void* ocur,
                                             Stamps* st) {
@@ -386,14 +463,21 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
 #pragma unroll
         for (int q = 0; q < Q; ++q) twiddle_bases<T, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
 #endif
-        __syncthreads();                       // earlier readers of the image are done
+        lds_barrier();                         // earlier readers of the image are done
         lds_write<T, N, E, P - 1, 0>(v, lds, t);
-        __syncthreads();
+        lds_barrier();
         lds_read<T, N, E, P, 0>(v, lds, t);
-        __syncthreads();
+        lds_barrier();
         lds_write<T, N, E, P - 1, 1>(v, lds, t);
-        __syncthreads();
+        lds_barrier();
         lds_read<T, N, E, P, 1>(v, lds, t);
+        if constexpr (I::LAST && XD) {
+            if (xs_next) {                     // the image is idle once every wave has read it
+                lds_barrier();
+                dma_x<N, Geometry<N, E>::T>(reinterpret_cast<const C2<float>*>(xs_next), lds, t);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
         drain<T, N, E, OUT, 2 * P - 1>(o, oprev, t);
         NW_STAMP(st, 2 * P - 1);               // exchange P-1 -> P
 #pragma unroll
@@ -410,7 +494,9 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
                 drain<T, N, E, OUT, 2 * P + 1>(o, oprev, t);
                 drain<T, N, E, OUT, 2 * P + 2>(o, oprev, t);
             }
+#if NW_XPREFETCH
             if (xs_next) load_x<T, N, E>(x, xs_next, t, interp);
+#endif
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (NW_DEFER) {
 #pragma unroll
@@ -420,7 +506,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
             }
         } else {
             drain<T, N, E, OUT, 2 * P>(o, oprev, t);
-            passes_from<T, N, E, OUT, P + 1>(v, lds, t, tw, x, xs_next, interp, o, oprev, ocur, st);
+            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, interp, o, oprev, ocur, st);
         }
     }
 }
@@ -449,6 +535,11 @@ __device__ __forceinline__ void load_x(C2<T>* x, const C2<T>* xs, int t, bool in
     }
 }
 
+template <typename T, bool REALW>
+__device__ __forceinline__ auto wsel(cplx<T> w) {
+    if constexpr (REALW) return w.re; else return C2<T>{w.re, w.im};
+}
+
 template <typename T, bool REALW> struct WLoad;
 template <typename T> struct WLoad<T, true> {     // analytic wavelets: real rows
     using type = T;
@@ -467,13 +558,16 @@ constexpr int kTileF = 8;   // scales per XCD tile
 constexpr int kTileG = 8;   // signal groups per XCD tile
 
 #ifndef NW_WPS32
-#define NW_WPS32 2
+#define NW_WPS32 4
 #endif
 #ifndef NW_WPS16
 #define NW_WPS16 4
 #endif
 // fp64 holds twice the registers per element: 2 waves per SIMD
-#define NW_WAVES_PER_SIMD(T, E) (sizeof(T) == 8 || (E) >= 32 ? NW_WPS32 : NW_WPS16)
+#ifndef NW_WPS64
+#define NW_WPS64 2
+#endif
+#define NW_WAVES_PER_SIMD(T, E) (sizeof(T) == 8 ? NW_WPS64 : (E) >= 32 ? NW_WPS32 : NW_WPS16)
 template <typename T, int N, int E, int OUT, bool REALW>
 __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
                                                             const void* __restrict__ wtab, void* __restrict__ out,
@@ -481,6 +575,7 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
                                                             int nsg_pad) {
     using G = Geometry<N, E>;
     using WT = typename WLoad<T, REALW>::type;
+    constexpr bool XD = kXDMA<T, E, REALW>;
     extern __shared__ __align__(16) unsigned char smem[];
     T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
@@ -504,13 +599,21 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     // interpolate_alias zeroes X[k], k >= int(N/2); k = t + r*T >= N/2 exactly when r >= E/2
     const bool interp = d.xlim < N;
 
-    // W[f, k] at the thread's bins, evaluated once per block into registers (1/n folded in)
+    // W[f, k] at the thread's bins (1/n folded in).  NW_WMODE 0: evaluated once per block
+    // into registers; 1: read per signal from the device-built table (L2-shared by the
+    // XCD tile); 2: re-evaluated per signal (no registers held across signals).
+    const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * N;
+    const uint32_t wo = (uint32_t)t * (uint32_t)sizeof(WT);
+#if NW_WMODE == 0
     WT w[E];
 #pragma unroll
-    for (int r = 0; r < E; ++r) {
-        const cplx<T> wb = wavelet_bin<T>(d, fi, t + r * G::T);
-        if constexpr (REALW) w[r] = wb.re; else w[r] = C2<T>{wb.re, wb.im};
-    }
+    for (int r = 0; r < E; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
+#define NW_W_AT(r) w[r]
+#elif NW_WMODE == 1
+#define NW_W_AT(r) (*at(wrow, wo, (uint32_t)((r) * G::T * sizeof(WT))))
+#else
+#define NW_W_AT(r) wsel<T, REALW>(wavelet_bin<T>(d, fi, t + (r) * G::T))
+#endif
 
 #ifdef NW_STAMPS
     Stamps stamps{};
@@ -520,21 +623,59 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     Stamps* st = nullptr;
 #endif
     C2<T> x[E];
-    C2<T> o[E];                    // outputs of the previous signal, stored during this one
+    C2<T> o[E];                    // outputs of the previous signal, stored during this one (NW_DEFER)
     void* oprev = nullptr;
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T));
-    load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s_begin * d.nh), t, interp);
+    // XDMA: X[N/2] (the real Nyquist bin, outside the DMA'd half) of the signal being
+    // transformed, carried one signal ahead in registers so its load never queues behind
+    // a store and is never folded into a private/LDS pointer select
+    C2<T> nyq{T(0), T(0)};
+    if constexpr (XD) {
+        nyq = reinterpret_cast<const C2<T>*>(X + s_begin * d.nh)[N / 2];
+        dma_x<N, G::T>(reinterpret_cast<const C2<float>*>(X + s_begin * d.nh), lds, t);
+    } else {
+#if NW_XPREFETCH
+        load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s_begin * d.nh), t, interp);
+#endif
+    }
     for (int64_t s = s_begin; s < s_end; ++s) {
+        if constexpr (XD) {
+            // this wave's DMA landed (only the stores issued after it may be pending),
+            // then every wave's: the whole X[0 .. N/2) is in the image
+            if (s == s_begin) wait_vmcnt<0>(); else wait_vmcnt<LastStores<T, N, E, OUT>::COUNT>();
+            lds_barrier();
+            const C2<T>* xl = reinterpret_cast<const C2<T>*>(lds);
+            // X[N - k] for r >= E/2 from ONE base (the lowest address, r = E-1) and positive
+            // immediate offsets: DS offsets are unsigned, so N - t - r*T per r would hold E/2
+            // address registers
+            const C2<T>* xm = xl + (N - (E - 1) * G::T - t);
+#pragma unroll
+            for (int r = 0; r < E; ++r) {
+                if (r < E / 2) {
+                    x[r] = xl[t + r * G::T];
+                } else {                        // X[N - k]; k = N/2 (t = 0, r = E/2) is the Nyquist bin
+                    x[r] = xm[(E - 1 - r) * G::T];  // value copies: `c ? nyq : xl[m]` is an
+                    if (r == E / 2 && t == 0) x[r] = nyq;   // lvalue select (nyq -> scratch)
+                    x[r].im = -x[r].im;
+                }
+                if (r >= E / 2 && interp) x[r] = C2<T>{T(0), T(0)};
+            }
+            if (s + 1 < s_end) nyq = reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh)[N / 2];
+        } else {
+#if !NW_XPREFETCH
+            load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s * d.nh), t, interp);
+#endif
+        }
         // pass 0 (Ns = 1): z = W * X at k = t + r*T, radix-E IDFT in registers
         C2<T> v[E];
 #pragma unroll
-        for (int r = 0; r < E; ++r) v[r] = WLoad<T, REALW>::apply(w[r], x[r]);
+        for (int r = 0; r < E; ++r) v[r] = WLoad<T, REALW>::apply(NW_W_AT(r), x[r]);
         idft_br<T, E>(v);
         drain<T, N, E, OUT, 0>(o, oprev, t);
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
         void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
-        passes_from<T, N, E, OUT, 1>(v, lds, t, tw, x, xs_next, interp, o, oprev, ocur, st);
+        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, interp, o, oprev, ocur, st);
         oprev = ocur;
     }
     // the last signal's outputs
