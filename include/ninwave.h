@@ -58,6 +58,14 @@ extern "C" {
 #define NW_OUT_CWT   0   /* complex (S, F, N)   base.py:378-407 */
 #define NW_OUT_ABS   1   /* real    (S, F, N)   base.py:427-443 */
 #define NW_OUT_POWER 2   /* real    (S, F, N)   base.py:409-425 */
+/* Reductions over the nsig signals (EpochsWavelet, mneutils.py:42-71): out is (F, N),
+ * summed in signal order in fp64 on the device; (E, F, N) is never materialised. */
+#define NW_OUT_POWER_MEAN 3  /* real (F, N), compute dtype: mean_s |y|^2    mneutils.py:42-55 */
+#define NW_OUT_ITC        4  /* real (F, N), compute dtype: |mean_s y/|y||  mneutils.py:57-71;
+                                |y| = 0 gives NaN, as 0/0 does in the reference */
+#define NW_OUT_POWER_SUM  5  /* float64 (F, N): sum_s |y|^2 (partial sums to combine over
+                                devices or ranks, then divide by the total count) */
+#define NW_OUT_PHASE_SUM  6  /* complex128 (F, N): sum_s y/|y| (partial sums; ITC = |sum/S|) */
 
 /* memory placement of x / out in nw_execute */
 #define NW_MEM_HOST   0
@@ -128,13 +136,16 @@ int nw_plan_set_wavelet(nw_plan* plan, int kind, const double* params, int npara
 int nw_plan_wavelet_rows(nw_plan* plan, void* out_host);
 
 /* Run the CWT of nsig signals x[nsig][n] (plan dtype) into out[nsig][nfreq][n]
- * (complex for NW_OUT_CWT, real otherwise).  mem = NW_MEM_HOST: synchronous;
+ * (complex for NW_OUT_CWT, real otherwise), or (F, N) for the reduction kinds
+ * NW_OUT_POWER_MEAN .. NW_OUT_PHASE_SUM.  mem = NW_MEM_HOST: synchronous;
  * NW_MEM_DEVICE: x/out are device pointers on the plan's device, the call is
  * asynchronous on the plan stream (see nw_plan_sync). */
 int nw_execute(nw_plan* plan, const void* x, int64_t nsig, void* out, int out_kind, int mem);
 
 /* Shard nsig host signals over ndev plans (one per device, identical config),
- * one host thread per device; contiguous blocks of signals per device. */
+ * one host thread per device; contiguous blocks of signals per device.  For the
+ * reduction kinds each device sums its block and the host adds the fp64 partial
+ * sums in device order before the mean / |.| of the result. */
 int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t nsig,
                      void* out, int out_kind);
 

@@ -25,7 +25,7 @@ import numpy as np
 from scipy.fftpack import fft, ifft
 
 from . import _lib as L
-from .engine import Plan, execute_multi, np_dtype
+from .engine import REDUCTIONS, Plan, execute_multi, np_dtype
 
 # Device working-set budget per plan chunk (bytes); signals are streamed through it.
 CHUNK_BYTES = int(os.environ.get('NINWAVE_CHUNK_BYTES', str(4 << 30)))
@@ -262,6 +262,8 @@ class WaveletBase:
             per = -(-nsig // len(devs))
             plans = [self._plan(n, per, d) for d in devs]
             out = execute_multi(plans, x.reshape(nsig, n), out_kind)
+            if out_kind in REDUCTIONS:
+                return out
             return out.reshape(x.shape[:-1] + out.shape[-2:])
         return self._plan(n, nsig, devs[0]).execute(x, out_kind=out_kind)
 
@@ -311,7 +313,9 @@ class WaveletBase:
 
     def cwt_batch(self, waves: np.ndarray, freqs=None, reuse: bool = True,
                   out: str = 'cwt') -> np.ndarray:
-        """Batched CWT of (..., N) signals -> (..., F, N) in one device call.
+        """Batched CWT of (..., N) signals -> (..., F, N) in one device call, or (F, N)
+        for the reductions over all signals: ``power_mean``, ``itc`` (the compute
+        dtype), ``power_sum`` (float64) and ``phase_sum`` (complex128).
 
         Equivalent to stacking ``cwt(w, freqs, reuse)`` over the leading axes
         (the per-epoch loop of mneutils.py:39): the cache is built from the
@@ -321,8 +325,8 @@ class WaveletBase:
             raise ValueError('waves must have a trailing sample axis')
         if (not reuse) or self._cache is None:
             self._build_cache(freqs, waves.shape[-1] / self.sfreq)
-        if out not in ('cwt', 'abs', 'power'):
-            raise ValueError(f"out must be 'cwt', 'abs' or 'power', got {out!r}")
+        if out not in ('cwt', 'abs', 'power') + REDUCTIONS:
+            raise ValueError(f"out must be one of cwt, abs, power, {', '.join(REDUCTIONS)}; got {out!r}")
         return self._run(waves, out)
 
     def plan_stats(self) -> list:

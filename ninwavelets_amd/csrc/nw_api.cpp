@@ -100,6 +100,8 @@ struct nw_plan {
     size_t d_Y_bytes = 0;
     void* d_out = nullptr;
     size_t d_out_bytes = 0;
+    void* d_acc = nullptr;           // epoch reductions: fp64 (F, n) sums (x2 for phases)
+    size_t d_acc_bytes = 0;
     void* d_wtab = nullptr;          // fused engine: W[f, k] (pad_to + 1/n applied)
     size_t d_wtab_bytes = 0;
     bool wtab_valid = false;
@@ -179,37 +181,31 @@ rocfft_precision prec(const nw_plan* p) {
     return p->dtype == NW_F32 ? rocfft_precision_single : rocfft_precision_double;
 }
 
-int get_rocfft_plans(nw_plan* p, int64_t batch, rocfft_plan* fwd, rocfft_plan* inv) {
-    auto itf = p->fwd.find(batch);
-    if (itf == p->fwd.end()) {
+// rocFFT plans keyed by batch count: R2C forward over signals, C2C inverse (in place)
+// over (signal, scale) rows.
+int get_plan(nw_plan* p, bool inverse, int64_t batch, rocfft_plan* out) {
+    auto& m = inverse ? p->inv : p->fwd;
+    auto it = m.find(batch);
+    if (it == m.end()) {
         size_t len = (size_t)p->n;
-        rocfft_plan pf = nullptr;
-        NW_RF(rocfft_plan_create(&pf, rocfft_placement_notinplace, rocfft_transform_type_real_forward, prec(p), 1,
-                                 &len, (size_t)batch, nullptr));
-        p->fwd[batch] = pf;
+        rocfft_plan pl = nullptr;
+        NW_RF(rocfft_plan_create(&pl, inverse ? rocfft_placement_inplace : rocfft_placement_notinplace,
+                                 inverse ? rocfft_transform_type_complex_inverse : rocfft_transform_type_real_forward,
+                                 prec(p), 1, &len, (size_t)batch, nullptr));
+        m[batch] = pl;
         size_t ws = 0;
-        NW_RF(rocfft_plan_get_work_buffer_size(pf, &ws));
+        NW_RF(rocfft_plan_get_work_buffer_size(pl, &ws));
         if (ws > p->work_bytes) NW_TRY(ensure(&p->work, &p->work_bytes, ws));
-        itf = p->fwd.find(batch);
+        it = m.find(batch);
     }
-    *fwd = itf->second;
-    if (inv) {
-        auto iti = p->inv.find(batch);
-        if (iti == p->inv.end()) {
-            size_t len = (size_t)p->n;
-            rocfft_plan pi = nullptr;
-            NW_RF(rocfft_plan_create(&pi, rocfft_placement_inplace, rocfft_transform_type_complex_inverse, prec(p), 1,
-                                     &len, (size_t)(batch * p->nfreq), nullptr));
-            p->inv[batch] = pi;
-            size_t ws = 0;
-            NW_RF(rocfft_plan_get_work_buffer_size(pi, &ws));
-            if (ws > p->work_bytes) NW_TRY(ensure(&p->work, &p->work_bytes, ws));
-            iti = p->inv.find(batch);
-        }
-        *inv = iti->second;
-    }
+    *out = it->second;
     return NW_OK;
 }
+
+// One rocFFT execution covers at most 2^31 elements: a single 512 x 2^24 batch
+// (C5, 8.6e9 elements) completes only part of its rows, so longer batches run as
+// several executions of <= kFftElems / n rows each.
+constexpr int64_t kFftElems = int64_t(1) << 31;
 
 int run_fft(nw_plan* p, rocfft_plan plan, void* in, void* out) {
     NW_RF(rocfft_execution_info_set_stream(p->info, p->stream));
@@ -220,18 +216,38 @@ int run_fft(nw_plan* p, rocfft_plan plan, void* in, void* out) {
     return NW_OK;
 }
 
+// The rocFFT engine's Y buffer (max_batch x F x n complex) is allocated on first need:
+// a device-output CWT writes Y straight into the caller's buffer and never needs it
+// (at C5, 512 x 2^24 complex64 = 68.7 GB of HBM saved).
+int need_Y(nw_plan* p) {
+    return ensure(&p->d_Y, &p->d_Y_bytes, (size_t)p->max_batch * p->nfreq * p->n * 2 * p->esz);
+}
+
 // One device chunk: xs (device, c signals) -> dst (device).
+// rows transforms of length n starting at in/out (elem bytes per input / output element)
+int run_fft_rows(nw_plan* p, bool inverse, int64_t rows, char* in, char* out, size_t in_row, size_t out_row) {
+    const int64_t group = std::max<int64_t>(1, kFftElems / p->n);
+    for (int64_t r0 = 0; r0 < rows; r0 += group) {
+        const int64_t nb = std::min<int64_t>(group, rows - r0);
+        rocfft_plan pl = nullptr;
+        NW_TRY(get_plan(p, inverse, nb, &pl));
+        NW_TRY(run_fft(p, pl, in + r0 * in_row, out ? out + r0 * out_row : nullptr));
+    }
+    return NW_OK;
+}
+
 int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
-    rocfft_plan fwd = nullptr, inv = nullptr;
     const bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
-    NW_TRY(get_rocfft_plans(p, c, &fwd, rocfft_engine ? &inv : nullptr));
     // rocFFT may use its input as scratch: transform from the plan's own copy.
     if (xs_dev != p->d_x)
         NW_TRY(staged(p, ST_COPY, [&] {
             NW_HIP(hipMemcpyAsync(p->d_x, xs_dev, (size_t)c * p->n * p->esz, hipMemcpyDeviceToDevice, p->stream));
             return NW_OK;
         }));
-    NW_TRY(staged(p, ST_FWD, [&] { return run_fft(p, fwd, p->d_x, p->d_X); }));
+    NW_TRY(staged(p, ST_FWD, [&] {
+        return run_fft_rows(p, false, c, (char*)p->d_x, (char*)p->d_X, (size_t)p->n * p->esz,
+                            (size_t)p->nh * 2 * p->esz);
+    }));
 
     if (!rocfft_engine) {
         if (!p->wtab_valid) {
@@ -247,12 +263,19 @@ int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind
     }
     // K1 writes the product straight into the destination when the caller wants
     // the complex CWT on the device; otherwise into the plan's Y buffer.
-    void* Y = (out_kind == NW_OUT_CWT && dst_is_final) ? dst : p->d_Y;
+    void* Y = dst;
+    if (!(out_kind == NW_OUT_CWT && dst_is_final)) {
+        NW_TRY(need_Y(p));
+        Y = p->d_Y;
+    }
     NW_TRY(staged(p, ST_MUL, [&] {
         NW_HIP(nw::launch_multiply(p->desc, p->dtype, p->d_X, Y, c, p->stream));
         return NW_OK;
     }));
-    NW_TRY(staged(p, ST_INV, [&] { return run_fft(p, inv, Y, nullptr); }));
+    NW_TRY(staged(p, ST_INV, [&] {
+        const size_t row = (size_t)p->n * 2 * p->esz;
+        return run_fft_rows(p, true, c * p->nfreq, (char*)Y, nullptr, row, row);
+    }));
     if (out_kind == NW_OUT_CWT) {
         if (Y != dst)
             NW_TRY(staged(p, ST_COPY, [&] {
@@ -268,12 +291,74 @@ int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind
     });
 }
 
+bool is_reduction(int out_kind) { return out_kind >= NW_OUT_POWER_MEAN && out_kind <= NW_OUT_PHASE_SUM; }
+bool is_phase(int out_kind) { return out_kind == NW_OUT_ITC || out_kind == NW_OUT_PHASE_SUM; }
+
+// Epoch reductions (mneutils.py:42-71): every chunk's per-signal results (|y|^2 from
+// the fused kernel, or y from the rocFFT engine's Y / the fused CWT for phases) are
+// added in signal order into the fp64 accumulator; the (S, F, n) result never exists
+// beyond one chunk.  nsig = 0 leaves acc = 0, so the mean is 0/0 = NaN like
+// np.mean over an empty axis.
+int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind, bool host) {
+    const bool phase = is_phase(out_kind);
+    const int64_t fn = (int64_t)p->nfreq * p->n;
+    const size_t acc_bytes = (size_t)fn * (phase ? 2 : 1) * sizeof(double);
+    NW_TRY(ensure(&p->d_acc, &p->d_acc_bytes, acc_bytes));
+    NW_HIP(hipMemsetAsync(p->d_acc, 0, acc_bytes, p->stream));
+    const bool fused = p->engine == NW_ENGINE_FUSED;
+    const int sig_kind = (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
+    const int src_kind = phase ? nw::ACC_PHASE_Y : (fused ? nw::ACC_POWER_REAL : nw::ACC_POWER_Y);
+    void* scratch = nullptr;            // rocFFT engine: run_chunk leaves y in d_Y
+    if (!fused) {
+        NW_TRY(need_Y(p));
+        scratch = p->d_Y;
+    } else {
+        NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * fn * (phase ? 2 : 1) * p->esz));
+        scratch = p->d_out;
+    }
+    for (int64_t s0 = 0; s0 < nsig; s0 += p->max_batch) {
+        const int64_t c = std::min<int64_t>(p->max_batch, nsig - s0);
+        const void* xs = (const char*)x + (size_t)s0 * p->n * p->esz;
+        if (host) {
+            NW_TRY(staged(p, ST_COPY, [&] {
+                NW_HIP(hipMemcpyAsync(p->d_x, xs, (size_t)c * p->n * p->esz, hipMemcpyHostToDevice, p->stream));
+                return NW_OK;
+            }));
+            xs = p->d_x;
+        }
+        NW_TRY(run_chunk(p, xs, c, scratch, sig_kind, false));
+        NW_TRY(staged(p, ST_EPI, [&] {
+            NW_HIP(nw::launch_accumulate(p->dtype, src_kind, scratch, (double*)p->d_acc, fn, c, p->stream));
+            return NW_OK;
+        }));
+        p->stats.chunks++;
+    }
+    const hipMemcpyKind back = host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    if (out_kind == NW_OUT_POWER_SUM || out_kind == NW_OUT_PHASE_SUM) {
+        NW_HIP(hipMemcpyAsync(out, p->d_acc, acc_bytes, back, p->stream));
+    } else {
+        // scratch is >= fn elements of the plan dtype on both engines
+        void* dst = host ? scratch : out;
+        NW_TRY(staged(p, ST_EPI, [&] {
+            NW_HIP(nw::launch_finalize(p->dtype, phase, (const double*)p->d_acc, dst, fn, nsig, p->stream));
+            return NW_OK;
+        }));
+        if (host) NW_HIP(hipMemcpyAsync(out, dst, (size_t)fn * p->esz, hipMemcpyDeviceToHost, p->stream));
+    }
+    p->stats.executes++;
+    if (host) {
+        NW_HIP(hipStreamSynchronize(p->stream));
+        NW_TRY(resolve_timing(p));
+    }
+    return NW_OK;
+}
+
 void free_plan(nw_plan* p) {
     for (auto& kv : p->fwd) rocfft_plan_destroy(kv.second);
     for (auto& kv : p->inv) rocfft_plan_destroy(kv.second);
     if (p->info) rocfft_execution_info_destroy(p->info);
     void* bufs[] = {p->work,   p->d_x,    p->d_X,        p->d_Y,     p->d_out,      p->d_wtab,
-                    p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len};
+                    p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len, p->d_acc};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& pe : p->pending) {
@@ -384,10 +469,6 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     sz = 0;
     r = ensure(&p->d_X, &sz, (size_t)max_batch * p->nh * 2 * p->esz);
     if (r != NW_OK) return bail(r);
-    if (p->engine == NW_ENGINE_ROCFFT) {
-        r = ensure(&p->d_Y, &p->d_Y_bytes, (size_t)max_batch * nfreq * n * 2 * p->esz);
-        if (r != NW_OK) return bail(r);
-    }
     if (p->engine == NW_ENGINE_FUSED) {
         e = nw::fused_prepare(n, dtype);
         if (e != hipSuccess) return bail(fail(NW_E_HIP, std::string("fused_prepare: ") + hipGetErrorString(e)));
@@ -506,10 +587,11 @@ int nw_plan_wavelet_rows(nw_plan* p, void* out_host) {
 int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind, int mem) {
     if (!p || (!x && nsig > 0) || (!out && nsig > 0)) return fail(NW_E_INVALID, "nw_execute: null argument");
     if (!p->has_wavelet) return fail(NW_E_STATE, "nw_execute: nw_plan_set_wavelet first");
-    if (out_kind < NW_OUT_CWT || out_kind > NW_OUT_POWER) return fail(NW_E_INVALID, "nw_execute: bad out_kind");
+    if (out_kind < NW_OUT_CWT || out_kind > NW_OUT_PHASE_SUM) return fail(NW_E_INVALID, "nw_execute: bad out_kind");
     if (mem != NW_MEM_HOST && mem != NW_MEM_DEVICE) return fail(NW_E_INVALID, "nw_execute: bad mem");
     if (nsig < 0) return fail(NW_E_INVALID, "nw_execute: nsig < 0");
-    if (nsig == 0) return NW_OK;
+    if (is_reduction(out_kind) && !out) return fail(NW_E_INVALID, "nw_execute: null out");
+    if (nsig == 0 && !is_reduction(out_kind)) return NW_OK;
     DeviceGuard guard(p->device);
     // execute-time geometry: pad_to the cached rows to n, mask X (base.py:396-401)
     nw::WDesc& d = p->desc;
@@ -519,12 +601,15 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     d.off = d.len_full < p->n ? (p->n - d.len_full) / 2 : 0;
     d.xlim = (p->flags & NW_INTERPOLATE) ? p->n / 2 : p->n;   // int(n / 2) (base.py:120)
 
+    if (is_reduction(out_kind)) return execute_reduce(p, x, nsig, out, out_kind, mem == NW_MEM_HOST);
+
     const size_t out_elem = (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
     const size_t row_out = (size_t)p->nfreq * p->n * out_elem;  // one signal's output bytes
     const bool host = mem == NW_MEM_HOST;
     if (host && out_kind != NW_OUT_CWT && p->engine == NW_ENGINE_ROCFFT)
         NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * row_out));
     if (host && p->engine == NW_ENGINE_FUSED) NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * row_out));
+    if (host && p->engine == NW_ENGINE_ROCFFT && out_kind == NW_OUT_CWT) NW_TRY(need_Y(p));
     // (rocFFT engine, host CWT: the complex result is read back straight from d_Y)
 
     for (int64_t s0 = 0; s0 < nsig; s0 += p->max_batch) {
@@ -553,6 +638,53 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     return NW_OK;
 }
 
+// Reductions over devices: each device sums its contiguous block (fp64 partial sums),
+// the host adds them in device order, then takes the mean / |mean| exactly as
+// k_finalize does.
+static int execute_multi_reduce(nw_plan* const* plans, int nplans, const void* x, int64_t nsig, void* out,
+                                int out_kind) {
+    const nw_plan* p0 = plans[0];
+    const bool phase = is_phase(out_kind);
+    const int64_t fn = (int64_t)p0->nfreq * p0->n;
+    const size_t comps = (size_t)fn * (phase ? 2 : 1);
+    const size_t x_row = (size_t)p0->n * p0->esz;
+    const int64_t per = (nsig + nplans - 1) / nplans;
+    std::vector<std::vector<double>> part(nplans);
+    std::vector<int> rc(nplans, NW_OK);
+    std::vector<std::string> err(nplans);
+    std::vector<std::thread> th;
+    for (int i = 0; i < nplans; ++i) {
+        const int64_t s0 = std::min<int64_t>(nsig, (int64_t)i * per);
+        const int64_t cnt = std::min<int64_t>(nsig, s0 + per) - s0;
+        if (cnt <= 0) continue;
+        part[i].assign(comps, 0.0);
+        th.emplace_back([&, i, s0, cnt] {
+            rc[i] = nw_execute(plans[i], (const char*)x + s0 * x_row, cnt, part[i].data(),
+                               phase ? NW_OUT_PHASE_SUM : NW_OUT_POWER_SUM, NW_MEM_HOST);
+            if (rc[i] != NW_OK) err[i] = g_last_error;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int i = 0; i < nplans; ++i)
+        if (rc[i] != NW_OK) return fail(rc[i], "device " + std::to_string(plans[i]->device) + ": " + err[i]);
+    std::vector<double> tot(comps, 0.0);
+    for (int i = 0; i < nplans; ++i)
+        for (size_t j = 0; j < part[i].size(); ++j) tot[j] += part[i][j];
+    if (out_kind == NW_OUT_POWER_SUM || out_kind == NW_OUT_PHASE_SUM) {
+        std::memcpy(out, tot.data(), comps * sizeof(double));
+        return NW_OK;
+    }
+    const double d = (double)nsig;
+    for (int64_t j = 0; j < fn; ++j) {
+        const double v = phase ? std::hypot(tot[2 * j] / d, tot[2 * j + 1] / d) : tot[j] / d;
+        if (p0->dtype == NW_F32)
+            static_cast<float*>(out)[j] = (float)v;
+        else
+            static_cast<double*>(out)[j] = v;
+    }
+    return NW_OK;
+}
+
 int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t nsig, void* out, int out_kind) {
     if (!plans || nplans < 1) return fail(NW_E_INVALID, "nw_execute_multi: no plans");
     for (int i = 1; i < nplans; ++i)
@@ -560,6 +692,8 @@ int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t n
             plans[i]->dtype != plans[0]->dtype)
             return fail(NW_E_INVALID, "nw_execute_multi: plans must share n, nfreq and dtype");
     const nw_plan* p0 = plans[0];
+    if (out_kind < NW_OUT_CWT || out_kind > NW_OUT_PHASE_SUM) return fail(NW_E_INVALID, "nw_execute_multi: bad out_kind");
+    if (is_reduction(out_kind)) return execute_multi_reduce(plans, nplans, x, nsig, out, out_kind);
     const size_t x_row = (size_t)p0->n * p0->esz;
     const size_t o_row = (size_t)p0->nfreq * p0->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p0->esz;
     const int64_t per = (nsig + nplans - 1) / nplans;

@@ -124,6 +124,12 @@ __device__ __forceinline__ cplx<T> spectrum_bin(const cplx<T>* __restrict__ Xs, 
 hipError_t launch_multiply(const WDesc& d, int dtype, const void* X, void* Y, int64_t nsig, hipStream_t s);
 hipError_t launch_epilogue(int dtype, int out_kind, const void* Y, void* out, int64_t count, hipStream_t s);
 hipError_t launch_rows(const WDesc& d, int dtype, void* rows, hipStream_t s);
+// epoch reductions: source kinds of launch_accumulate
+enum { ACC_POWER_REAL = 0, ACC_POWER_Y = 1, ACC_PHASE_Y = 2 };
+hipError_t launch_accumulate(int dtype, int src_kind, const void* src, double* acc, int64_t fn, int64_t c,
+                             hipStream_t s);
+hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, int64_t fn, int64_t nsig,
+                           hipStream_t s);
 // fused engine (nw_fused.hip)
 bool       fused_supported(int64_t n, int dtype);
 hipError_t fused_prepare(int64_t n, int dtype);

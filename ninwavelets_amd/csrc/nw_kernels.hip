@@ -2,6 +2,7 @@
 //   K1  spectrum multiply  Y[s,f,k] = W[f,k] * X[s,k] / n      (base.py:396-406)
 //   K2  epilogue           |Y| or |Y|^2                          (base.py:409-443)
 //   rows                   the cached wavelet rows themselves     (base.py:221-279)
+//   accumulate / finalize  epoch reductions power / ITC          (mneutils.py:42-71)
 //
 // K1 is HBM-write bound (8 or 16 B per output point, X re-read from L2): each
 // block evaluates W for one scale f and a 256*V-bin tile ONCE into registers,
@@ -121,6 +122,91 @@ hipError_t launch_rows(const WDesc& d, int dtype, void* rows, hipStream_t s) {
         k_rows<float><<<grid, 256, 0, s>>>(d, (float*)rows);
     else
         k_rows<double><<<grid, 256, 0, s>>>(d, (double*)rows);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Epoch reductions (mneutils.py:42-71).  acc[f, k] (fp64) += the chunk's signals in
+// signal order -- numpy's np.mean(axis=0) adds the (F, N) slabs one after another,
+// then divides by the count.  One thread per (f, k), coalesced across k; each
+// signal's slab is S_STRIDE = F*n elements further on.
+//   ACC_POWER_REAL : src = |y|^2 (real T, the fused kernel's power output)
+//   ACC_POWER_Y    : src = y (complex T)  -> |y|^2
+//   ACC_PHASE_Y    : src = y (complex T)  -> y/|y| in fp64; 0/0 -> NaN (mneutils.py:68)
+// ---------------------------------------------------------------------------
+template <typename T, int SRC>
+__global__ __launch_bounds__(256) void k_accumulate(const void* __restrict__ src, double* __restrict__ acc,
+                                                    int64_t fn, int64_t c) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < fn; i += stride) {
+        if constexpr (SRC == ACC_PHASE_Y) {
+            double re = acc[2 * i], im = acc[2 * i + 1];
+            const cplx<T>* y = reinterpret_cast<const cplx<T>*>(src) + i;
+            for (int64_t s = 0; s < c; ++s) {
+                const cplx<T> v = y[s * fn];
+                const double a = hypot((double)v.re, (double)v.im);
+                re += (double)v.re / a;
+                im += (double)v.im / a;
+            }
+            acc[2 * i] = re;
+            acc[2 * i + 1] = im;
+        } else {
+            double p = acc[i];
+            for (int64_t s = 0; s < c; ++s) {
+                if constexpr (SRC == ACC_POWER_REAL) {
+                    p += (double)reinterpret_cast<const T*>(src)[s * fn + i];
+                } else {
+                    const cplx<T> v = reinterpret_cast<const cplx<T>*>(src)[s * fn + i];
+                    p += (double)v.re * (double)v.re + (double)v.im * (double)v.im;
+                }
+            }
+            acc[i] = p;
+        }
+    }
+}
+
+hipError_t launch_accumulate(int dtype, int src_kind, const void* src, double* acc, int64_t fn, int64_t c,
+                             hipStream_t s) {
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((fn + 255) / 256, 256 * 32));
+#define NW_ACC(T)                                                                                         \
+    switch (src_kind) {                                                                                   \
+        case ACC_POWER_REAL: k_accumulate<T, ACC_POWER_REAL><<<blocks, 256, 0, s>>>(src, acc, fn, c); break; \
+        case ACC_POWER_Y: k_accumulate<T, ACC_POWER_Y><<<blocks, 256, 0, s>>>(src, acc, fn, c); break;       \
+        default: k_accumulate<T, ACC_PHASE_Y><<<blocks, 256, 0, s>>>(src, acc, fn, c); break;               \
+    }
+    if (dtype == NW_F32) {
+        NW_ACC(float)
+    } else {
+        NW_ACC(double)
+    }
+#undef NW_ACC
+    return hipGetLastError();
+}
+
+// mean = acc / nsig (np.mean's true_divide by the count); ITC = |(re, im) / nsig|
+template <typename T, bool ITC>
+__global__ __launch_bounds__(256) void k_finalize(const double* __restrict__ acc, T* __restrict__ out, int64_t fn,
+                                                  double nsig) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < fn; i += stride) {
+        if constexpr (ITC)
+            out[i] = (T)hypot(acc[2 * i] / nsig, acc[2 * i + 1] / nsig);
+        else
+            out[i] = (T)(acc[i] / nsig);
+    }
+}
+
+hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, int64_t fn, int64_t nsig,
+                           hipStream_t s) {
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((fn + 255) / 256, 256 * 32));
+    const double d = (double)nsig;
+    if (dtype == NW_F32) {
+        if (itc) k_finalize<float, true><<<blocks, 256, 0, s>>>(acc, (float*)out, fn, d);
+        else k_finalize<float, false><<<blocks, 256, 0, s>>>(acc, (float*)out, fn, d);
+    } else {
+        if (itc) k_finalize<double, true><<<blocks, 256, 0, s>>>(acc, (double*)out, fn, d);
+        else k_finalize<double, false><<<blocks, 256, 0, s>>>(acc, (double*)out, fn, d);
+    }
     return hipGetLastError();
 }
 

@@ -14,7 +14,11 @@ import numpy as np
 
 from . import _lib as L
 
-OUT_KINDS = {'cwt': L.NW_OUT_CWT, 'abs': L.NW_OUT_ABS, 'power': L.NW_OUT_POWER}
+OUT_KINDS = {'cwt': L.NW_OUT_CWT, 'abs': L.NW_OUT_ABS, 'power': L.NW_OUT_POWER,
+             # reductions over the signals -> (F, n) (EpochsWavelet, mneutils.py:42-71)
+             'power_mean': L.NW_OUT_POWER_MEAN, 'itc': L.NW_OUT_ITC,
+             'power_sum': L.NW_OUT_POWER_SUM, 'phase_sum': L.NW_OUT_PHASE_SUM}
+REDUCTIONS = ('power_mean', 'itc', 'power_sum', 'phase_sum')
 KINDS = {'morse': L.NW_MORSE, 'morlet': L.NW_MORLET, 'shannon': L.NW_SHANNON, 'table': L.NW_TABLE}
 
 
@@ -27,6 +31,10 @@ def np_dtype(dtype) -> np.dtype:
 
 def out_dtype(dtype, out_kind: str) -> np.dtype:
     dt = np_dtype(dtype)
+    if out_kind == 'power_sum':                 # fp64 partial sums whatever the compute dtype
+        return np.dtype(np.float64)
+    if out_kind == 'phase_sum':
+        return np.dtype(np.complex128)
     if out_kind == 'cwt':
         return np.dtype(np.complex64 if dt == np.float32 else np.complex128)
     return dt
@@ -92,6 +100,7 @@ class Plan:
     def execute(self, x, out=None, out_kind: str = 'cwt'):
         """x: (S, n) numpy array (host) -> returns (S, nfreq, n); or device tensors."""
         kind = OUT_KINDS[out_kind]
+        reduce = out_kind in REDUCTIONS
         if _is_device_tensor(x):
             if out is None:
                 raise ValueError('device execute needs an output tensor')
@@ -106,9 +115,10 @@ class Plan:
         lead = x.shape[:-1]
         nsig = int(np.prod(lead)) if lead else 1
         odt = out_dtype(self.dtype, out_kind)
+        shape = (self.nfreq, self.n) if reduce else lead + (self.nfreq, self.n)
         if out is None:
-            out = np.empty(lead + (self.nfreq, self.n), dtype=odt)
-        elif out.dtype != odt or not out.flags.c_contiguous or out.size != nsig * self.nfreq * self.n:
+            out = np.empty(shape, dtype=odt)
+        elif out.dtype != odt or not out.flags.c_contiguous or out.size != int(np.prod(shape)):
             raise ValueError('out must be a C-contiguous array of the right dtype and size')
         L.check(L.lib().nw_execute(self._h, x.ctypes.data_as(ctypes.c_void_p), nsig,
                                    out.ctypes.data_as(ctypes.c_void_p), kind, L.NW_MEM_HOST))
@@ -124,12 +134,17 @@ class Plan:
         want_x = torch.float32 if self.dtype == np.float32 else torch.float64
         want_o = {('cwt', np.float32): torch.complex64, ('cwt', np.float64): torch.complex128}.get(
             (out_kind, self.dtype.type), want_x)
+        if out_kind == 'power_sum':
+            want_o = torch.float64
+        elif out_kind == 'phase_sum':
+            want_o = torch.complex128
         if x.dtype != want_x or out.dtype != want_o:
             raise ValueError(f'device buffers must be {want_x} in / {want_o} out')
         if not (x.is_contiguous() and out.is_contiguous()):
             raise ValueError('device buffers must be contiguous')
-        if x.numel() != nsig * self.n or out.numel() != nsig * self.nfreq * self.n:
-            raise ValueError('device buffer sizes do not match (S, n) -> (S, nfreq, n)')
+        rows = 1 if out_kind in REDUCTIONS else nsig
+        if x.numel() != nsig * self.n or out.numel() != rows * self.nfreq * self.n:
+            raise ValueError('device buffer sizes do not match (S, n) -> (S, nfreq, n) / (nfreq, n)')
         if x.device.index != self.device or out.device.index != self.device:
             raise ValueError(f'device buffers must live on device {self.device}')
 
@@ -172,7 +187,8 @@ def execute_multi(plans, x: np.ndarray, out_kind: str = 'cwt') -> np.ndarray:
     x = np.ascontiguousarray(x, dtype=p0.dtype)
     lead = x.shape[:-1]
     nsig = int(np.prod(lead)) if lead else 1
-    out = np.empty(lead + (p0.nfreq, p0.n), dtype=out_dtype(p0.dtype, out_kind))
+    shape = (p0.nfreq, p0.n) if out_kind in REDUCTIONS else lead + (p0.nfreq, p0.n)
+    out = np.empty(shape, dtype=out_dtype(p0.dtype, out_kind))
     arr = (ctypes.c_void_p * len(plans))(*[p.handle.value for p in plans])
     L.check(L.lib().nw_execute_multi(arr, len(plans), x.ctypes.data_as(ctypes.c_void_p), nsig,
                                      out.ctypes.data_as(ctypes.c_void_p), OUT_KINDS[out_kind]))

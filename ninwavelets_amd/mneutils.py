@@ -29,12 +29,11 @@ class EpochsWavelet:
         return self.wavelet.cwt_batch(self._waves(ch_name), freqs, reuse=True)
 
     def power(self, ch_name: str, freqs) -> np.ndarray:
-        """Epoch-mean of |cwt|^2, (F, N) (mneutils.py:42-55)."""
-        p = self.wavelet.cwt_batch(self._waves(ch_name), freqs, reuse=True, out='power')
-        return np.mean(p, axis=0)
+        """Epoch-mean of |cwt|^2, (F, N) (mneutils.py:42-55), reduced on the device:
+        the (epochs, F, N) CWT is never materialised (fp64 sums in epoch order)."""
+        return self.wavelet.cwt_batch(self._waves(ch_name), freqs, reuse=True, out='power_mean')
 
     def itc(self, ch_name: str, freqs) -> np.ndarray:
-        """Inter-trial coherence |mean(cwt/|cwt|)|, (F, N) (mneutils.py:57-71)."""
-        c = self.cwt(ch_name, freqs)
-        with np.errstate(invalid='ignore', divide='ignore'):
-            return np.abs(np.mean(c / np.abs(c), axis=0))
+        """Inter-trial coherence |mean(cwt/|cwt|)|, (F, N) (mneutils.py:57-71), reduced
+        on the device; a point where some epoch has |cwt| = 0 is NaN, as in the reference."""
+        return self.wavelet.cwt_batch(self._waves(ch_name), freqs, reuse=True, out='itc')

@@ -216,3 +216,128 @@ def test_multi_plan_sharding_is_exact():
     single = plans[0].execute(x, out_kind='power')
     sharded = nw.execute_multi(plans, x, out_kind='power')
     np.testing.assert_array_equal(sharded, single)
+
+
+# ------------------------------------------------------------------ epoch reductions
+def _plan(n, F, dtype, freqs, engine=None, max_batch=8, kind='morse', params=(17.5, 3.)):
+    g = nw._lib.trans_grid(n / 1000., 1000., False)
+    p = nw.Plan(n, F, dtype, max_batch=max_batch, engine=None if engine == 'auto' else engine)
+    p.set_wavelet(kind, list(params), freqs, g)
+    return p
+
+
+@pytest.mark.parametrize('engine', ENGINES)
+@pytest.mark.parametrize('dtype', ['float64', 'float32'])
+def test_epoch_reductions_match_materialised(dtype, engine):
+    """power_mean / itc (mneutils.py:42-71) reduced on the device over 3 chunks equal the
+    reference formulas applied to the materialised CWT of the same plan; the fp64 sum
+    kinds are the un-normalised partials.  Tolerance: 1e-13 (fp64), 2e-6 (fp32: the fused
+    kernel's |y|^2 is rounded to fp32 before the fp64 sum)."""
+    n, F, S = 4096, 24, 21
+    x = synth(S, n, 21).astype(dtype)
+    freqs = np.linspace(2., 120., F)
+    plan = _plan(n, F, dtype, freqs, engine)
+    c = plan.execute(x, out_kind='cwt').astype(np.complex128)
+    ref_p = np.mean(np.abs(c) ** 2, axis=0)
+    ref_i = np.abs(np.mean(c / np.abs(c), axis=0))
+    t = 1e-13 if dtype == 'float64' else 2e-6
+    pm = plan.execute(x, out_kind='power_mean')
+    itc = plan.execute(x, out_kind='itc')
+    assert pm.shape == (F, n) and pm.dtype == np.dtype(dtype) and itc.dtype == np.dtype(dtype)
+    assert rel_err(pm, ref_p) <= t
+    assert np.max(np.abs(itc - ref_i)) <= t           # ITC lies in [0, 1]
+    ps = plan.execute(x, out_kind='power_sum')
+    ph = plan.execute(x, out_kind='phase_sum')
+    assert ps.dtype == np.float64 and ph.dtype == np.complex128
+    assert rel_err(ps / S, ref_p) <= t
+    assert np.max(np.abs(np.abs(ph / S) - ref_i)) <= t
+
+
+@pytest.mark.parametrize('engine', ENGINES)
+@pytest.mark.parametrize('dtype', ['float64', 'float32'])
+def test_itc_is_nan_where_an_epoch_is_zero(dtype, engine):
+    """An all-zero epoch has cwt == 0 exactly, so cwt/|cwt| is 0/0 = NaN in the reference
+    (mneutils.py:68) and the mean stays NaN; power ignores nothing."""
+    n, F, S = 1024, 8, 5
+    x = synth(S, n, 3).astype(dtype)
+    x[2] = 0
+    freqs = np.arange(1., F + 1)
+    plan = _plan(n, F, dtype, freqs, engine)
+    assert np.all(np.isnan(plan.execute(x, out_kind='itc')))
+    c = plan.execute(x, out_kind='cwt').astype(np.complex128)
+    assert np.all(c[2] == 0)
+    pm = plan.execute(x, out_kind='power_mean')
+    assert np.all(np.isfinite(pm)) and rel_err(pm, np.mean(np.abs(c) ** 2, axis=0)) <= 2e-6
+
+
+def test_epoch_reductions_empty_is_nan():
+    plan = _plan(256, 3, 'float64', np.array([1., 2., 3.]))
+    out = plan.execute(np.zeros((0, 256)), out_kind='power_mean')
+    assert out.shape == (3, 256) and np.all(np.isnan(out))     # 0/0, like np.mean over nothing
+
+
+def test_epoch_reductions_device_tensors_and_multi_plan():
+    torch = pytest.importorskip('torch')
+    n, F, S = 16384, 32, 12
+    x = synth(S, n, 13)
+    freqs = np.arange(1., F + 1)
+    plan = _plan(n, F, 'float32', freqs)
+    host = plan.execute(x, out_kind='power_mean')
+    xt = torch.from_numpy(x).cuda()
+    ot = torch.empty((F, n), dtype=torch.float32, device='cuda')
+    plan.execute(xt, ot, out_kind='power_mean')
+    plan.sync()
+    np.testing.assert_array_equal(ot.cpu().numpy(), host)     # same sums, same order
+    plans = [_plan(n, F, 'float32', freqs, max_batch=4) for _ in range(2)]
+    for kind in ('power_mean', 'itc'):
+        single = plan.execute(x, out_kind=kind)
+        sharded = nw.execute_multi(plans, x, out_kind=kind)
+        assert sharded.shape == (F, n)
+        assert np.max(np.abs(sharded - single)) <= 1e-6 * max(1.0, np.max(np.abs(single)))
+
+
+def test_epochs_wavelet_power_matches_per_epoch_reference():
+    """EpochsWavelet.power/itc (device reductions) against the reference formulas on the
+    oracle's per-epoch CWTs (mneutils.py:39, 53-55, 67-71)."""
+    E, n, freqs = 7, 2048, [3., 9., 27., 81.]
+    data = synth(E * 2, n, 31).astype(np.float64).reshape(E, 2, n)
+    ep = FakeEpochs(data, 1000., ['a', 'b'])
+    ref = np.array([O.cwt('morse', data[e, 1], freqs) for e in range(E)])
+    pw = nw.EpochsWavelet(ep, nw.Morse(1000)).power('b', freqs)
+    assert rel_err(pw, np.mean(np.abs(ref) ** 2, axis=0)) <= 1e-12
+    itc = nw.EpochsWavelet(ep, nw.Morse(1000)).itc('b', freqs)
+    assert np.max(np.abs(itc - np.abs(np.mean(ref / np.abs(ref), axis=0)))) <= 1e-10
+
+
+# ------------------------------------------------------------------ C5 scale (N = 2^24)
+@pytest.mark.parametrize('kind,dtype', [('morse', 'float32'), ('shannon', 'float64'), ('morse', 'float64')])
+def test_c5_scale_single_signal(kind, dtype):
+    """One 2^24-sample signal (the rocFFT engine) at three of C5's 512 scales against
+    the fp64 oracle.  Tolerance at this length: 1e-4 (fp32), 1e-12 (fp64)."""
+    n = 1 << 24
+    freqs = np.linspace(0.5, 250, 512)[[0, 200, 511]]
+    x = synth(1, n, 3)[0].astype(dtype)
+    out = CLASSES[kind](1000, dtype=dtype).cwt(x, freqs)
+    ref = O.cwt(kind, x.astype(np.float64), freqs)
+    assert out.shape == (3, n)
+    assert rel_err(out, ref) <= (1e-4 if dtype == 'float32' else 1e-12), rel_err(out, ref)
+
+
+def test_c5_all_512_scales_into_hbm():
+    """The whole C5 fp32 output (512 x 2^24 complex64 = 68.7 GB) written into one device
+    buffer (no Y staging buffer), sampled rows against the oracle."""
+    torch = pytest.importorskip('torch')
+    n, F = 1 << 24, 512
+    freqs = np.linspace(0.5, 250, F)
+    x = synth(1, n, 3)[0]
+    plan = _plan(n, F, 'float32', freqs, max_batch=1)
+    xt = torch.from_numpy(x).cuda()
+    ot = torch.empty((1, F, n), dtype=torch.complex64, device='cuda')
+    plan.execute(xt, ot, out_kind='cwt')
+    plan.sync()
+    sel = [0, 255, 511]
+    got = ot[0, sel].cpu().numpy()
+    del ot
+    torch.cuda.empty_cache()
+    ref = O.cwt('morse', x.astype(np.float64), freqs[sel])
+    assert rel_err(got, ref) <= 1e-4, rel_err(got, ref)
