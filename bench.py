@@ -118,6 +118,8 @@ def main():
     ap.add_argument('--engine', default='auto', choices=['auto', 'rocfft', 'fused'])
     ap.add_argument('--chunk', type=int, default=256, help='signals per device chunk')
     ap.add_argument('--epochs', type=int, default=None, help='override epochs per GPU')
+    ap.add_argument('--output', default=None, choices=['cwt', 'abs', 'power'],
+                    help='override the config\'s output kind (diagnostics)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 
@@ -138,6 +140,8 @@ def main():
     kind, epochs, chans, n, freqs, out_kind, dtype, text = CONFIGS[args.config]
     if args.epochs:
         epochs = args.epochs
+    if args.output:
+        out_kind = args.output
     S = epochs * chans                       # signals on this rank
     F = len(freqs)
     C = min(args.chunk, S)

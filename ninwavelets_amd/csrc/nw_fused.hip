@@ -25,6 +25,13 @@
 #ifndef NW_HWTWIDDLE
 #define NW_HWTWIDDLE 1   // fp32 twiddles from v_cos/v_sin (no loads); fp64 always uses the table
 #endif
+#ifndef NW_PACK_STORES
+#define NW_PACK_STORES 1   // unpaired last pass: lane-pair transposes -> 16-B stores
+#endif
+#ifndef NW_PACK_MAX
+#define NW_PACK_MAX 2      // measured (n = 4096): pairs of 8-B outputs 0.413 -> 0.403 ms (cwt);
+                           // quads of 4-B outputs 0.337 -> 0.360 ms (power): slower, so off
+#endif
 #ifndef NW_XDMA_MIN_E
 #define NW_XDMA_MIN_E 32 // fp32 with E >= this: the next signal's X copied into the idle LDS
                          // image by LDS-DMA before the stores (measured: E=32 1.99 -> 1.94 ms,
@@ -172,14 +179,19 @@ __device__ __forceinline__ void twiddle_apply(C2<T>* v, const C2<T>* p) {
     }
 }
 
-// Padded LDS half image (one real component at a time): 2 extra slots after
-// every E slots (E = elements per thread).  The pass-0 scatter (thread t owns
-// slots t*E .. t*E+E-1) then hits distinct banks with pair stores, pairs stay
-// aligned, and every later access is base(thread) + compile-time offset because
-// all strides are multiples of E.
-template <int E> __device__ __forceinline__ int lds_idx(int i) { return i + 2 * (i / E); }
-template <int E> constexpr int lds_off(int c) { return c + 2 * (c / E); }   // c a multiple of E
-template <int N, int E> constexpr int lds_elems() { return N + 2 * (N / E); }
+// Padded LDS half image (one real component at a time): 2 extra slots after every
+// kPadG<E> slots (E = elements per thread; 32 slots for E = 16, E otherwise).  Pairs
+// stay 8-B aligned, and every access is base(thread) + compile-time offset: bases
+// mod kPadG plus offsets mod kPadG never carry at the instantiated sizes (checked
+// exhaustively for N = 1024 .. 16384).  Padding every 16 slots at E = 16 made every
+// exchange access 2-way bank-conflicted (a contiguous 32-lane ds_read_b32 wrapped its
+// last two lanes onto banks 0-1; rocprofv3 SQ_LDS_BANK_CONFLICT = 2.2 cycles per LDS
+// instruction at C3); every 32 slots removes them at N = 4096 and leaves 1 in 8
+// elsewhere (bank model: MI355X_MICROARCH.md §LDS).
+template <int E> constexpr int kPadG = E < 32 ? 32 : E;
+template <int E> __device__ __forceinline__ int lds_idx(int i) { return i + 2 * (i / kPadG<E>); }
+template <int E> constexpr int lds_off(int c) { return c + 2 * (c / kPadG<E>); }   // c a multiple of E
+template <int N, int E> constexpr int lds_elems() { return N + 2 * (N / kPadG<E>); }
 
 template <int N, int E> struct Geometry {
     static constexpr int T = N / E;                 // threads per block
@@ -324,6 +336,35 @@ template <int N, int E, int P> struct PassInfo {
     __device__ static __forceinline__ int bfly(int t, int q) { return PAIRED ? Q * t + q : t + q * G::T; }
 };
 
+// Pass-1 twiddles w_{NS*R}^{(j % NS) * r} depend on j % NS only (NS = E, the pass-0
+// radix): an NS x (R-1) table in LDS after the image (7.75 KiB at n = 16384 fp32),
+// filled once per block from the exact global table, replaces that pass's v_sin/v_cos
+// bases and their products (the kernel is power-bound: every VALU op saved counts).
+#ifndef NW_TAB1
+#define NW_TAB1 1
+#endif
+template <typename T, int N, int E> struct Tab1 {
+    using I = PassInfo<N, E, 1>;
+    static constexpr int NS = I::NS, R = I::R;
+    static constexpr int COUNT = Geometry<N, E>::npass() >= 2 ? NS * (R - 1) : 0;
+    static constexpr bool ON = NW_TAB1 && COUNT > 0 && COUNT * (int)sizeof(C2<T>) <= 8192;
+    static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<T>) : 0;
+    static_assert((lds_elems<N, E>() * sizeof(T)) % 16 == 0, "table alignment");
+    __device__ static __forceinline__ const C2<T>* table(const T* lds) {
+        return reinterpret_cast<const C2<T>*>(lds + lds_elems<N, E>());
+    }
+    // w_N^e entries from the exact table tw (tw[i] = exp(+2 pi i / N))
+    __device__ static __forceinline__ void fill(T* lds, const C2<T>* __restrict__ tw, int t) {
+        if constexpr (ON) {
+            C2<T>* tab = reinterpret_cast<C2<T>*>(lds + lds_elems<N, E>());
+            for (int i = t; i < COUNT; i += Geometry<N, E>::T) {
+                const int jj = i % NS, r = i / NS + 1;
+                tab[i] = tw[(jj * r * (N / (NS * R))) % N];
+            }
+        }
+    }
+};
+
 template <typename T, int N, int E, int P, int COMP>
 __device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
     using I = PassInfo<N, E, P>;
@@ -369,9 +410,11 @@ __device__ __forceinline__ void lds_barrier() {
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef __attribute__((address_space(1))) void gbl_void_t;
 
-template <int N, int TT>
-__device__ __forceinline__ void dma_x(const C2<float>* xs, float* lds, int t) {
-    constexpr int CH = N * 4 / 16;                 // 16-byte chunks of X[0 .. N/2)
+// LDS-DMA of X[0 .. N/2) (the R2C half spectrum without its Nyquist bin) into LDS at dst:
+// 16 B per lane per instruction, wave w filling its own 1 KiB slices of each round.
+template <typename T, int N, int TT>
+__device__ __forceinline__ void dma_x(const C2<T>* xs, void* dst, int t) {
+    constexpr int CH = (N / 2) * (int)sizeof(C2<T>) / 16;   // 16-byte chunks
     static_assert(CH % TT == 0, "whole DMA rounds");
     const int wave_base = (t & ~63) * 16;
     const uint32_t lane_off = (uint32_t)t * 16u;
@@ -382,7 +425,7 @@ __device__ __forceinline__ void dma_x(const C2<float>* xs, float* lds, int t) {
         asm volatile("" : "+s"(chunk));           // computed here, in SGPRs (not hoisted)
         const char* src = at(chunk, lane_off);
         __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
-                                         (lds_void_t*)(reinterpret_cast<char*>(lds) + i * TT * 16 + wave_base), 16,
+                                         (lds_void_t*)(reinterpret_cast<char*>(dst) + i * TT * 16 + wave_base), 16,
                                          0, 0);
     }
 }
@@ -394,13 +437,85 @@ __device__ __forceinline__ void wait_vmcnt() {
     __builtin_amdgcn_s_waitcnt((V & 0xF) | ((V >> 4) << 14) | 0x70 | 0xF00);
 }
 
+// ---- lane-group transposes for the last pass's stores (DPP quad_perm, no LDS)
+template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+template <int CTRL> __device__ __forceinline__ double dpp_f(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// 2x2 transpose of (register a, register b) x (lane l, lane l ^ D): the lane with bit D
+// clear keeps a and takes its partner's a as b; the other keeps b and takes the partner's b as a
+template <int D, typename F> __device__ __forceinline__ void xpose2(F& a, F& b, bool hi) {
+    constexpr int CTRL = D == 1 ? 0xB1 : 0x4E;      // quad_perm [1,0,3,2] / [2,3,0,1]
+    const F recv = dpp_f<CTRL>(hi ? a : b);
+    if (hi) a = recv; else b = recv;
+}
+template <typename F> __device__ __forceinline__ void xpose2(C2<F>& a, C2<F>& b, bool hi, int d) {
+    if (d == 1) { xpose2<1>(a.re, b.re, hi); xpose2<1>(a.im, b.im, hi); }
+    else { xpose2<2>(a.re, b.re, hi); xpose2<2>(a.im, b.im, hi); }
+}
+
 // ---- the last pass's outputs: store number i (0 .. nstores-1) of a thread
+// Unpaired last pass (Q = 1: lane t owns outputs t + NS*m, NS apart): PACK lanes swap
+// PACK rows with a PACK x PACK transpose, so each lane stores PACK consecutive outputs
+// as ONE 16-B store -- 4x fewer store instructions for |y|^2 (fp32), 2x for y.  The
+// stores, not their bytes, limited these sizes (n = 4096: 2x the bytes of cwt over
+// power cost +20 % time).
 template <typename T, int N, int E, int OUT>
 struct LastStores {
     using I = PassInfo<N, E, Geometry<N, E>::npass() - 1>;
+    using O = typename OutT<OUT, T>::type;
     static constexpr int R = I::R, Q = I::Q;
     static constexpr int STEP = I::PAIRED ? 2 : 1;
-    static constexpr int COUNT = Q / STEP * R;      // store instructions per thread per signal
+    static constexpr int PACK_W = (int)(16 / sizeof(O));
+    static constexpr int PACK = (!I::PAIRED && Q == 1 && NW_PACK_STORES && PACK_W <= NW_PACK_MAX) ? PACK_W : 1;
+    static_assert(PACK == 1 || PACK == 2 || PACK == 4, "pack");
+    static constexpr int COUNT = PACK > 1 ? R / PACK : Q / STEP * R;   // store instructions per thread per signal
+    // all stores of one signal (v: the last pass's registers, bit-reversed rows)
+    __device__ static __forceinline__ void all(const C2<T>* v, void* orow, int t) {
+        if constexpr (PACK == 1) {
+            chunk<0, 1>(v, orow, t);
+        } else {
+            const int c = t & (PACK - 1);
+            const uint32_t lane = (uint32_t)((t & ~(PACK - 1)) + I::NS * c) * (uint32_t)sizeof(O);
+#pragma unroll
+            for (int g = 0; g < R / PACK; ++g) {
+                O val[PACK];
+#pragma unroll
+                for (int b = 0; b < PACK; ++b) val[b] = out_value<OUT, T>(v[bitrev<R>(g * PACK + b)]);
+                if constexpr (PACK >= 2) {
+                    const bool hi1 = c & 1;
+#pragma unroll
+                    for (int b = 0; b < PACK; b += 2) xpose_any<1>(val[b], val[b + 1], hi1);
+                }
+                if constexpr (PACK == 4) {
+                    const bool hi2 = c & 2;
+                    xpose_any<2>(val[0], val[2], hi2);
+                    xpose_any<2>(val[1], val[3], hi2);
+                }
+                using V = float __attribute__((ext_vector_type(4)));
+                struct alignas(16) P16 { O a[PACK]; };
+                P16 pk;
+#pragma unroll
+                for (int b = 0; b < PACK; ++b) pk.a[b] = val[b];
+#ifdef NW_ABL_NOSTORE
+                asm volatile("" ::"v"(__builtin_bit_cast(V, pk)));
+#else
+                __builtin_nontemporal_store(__builtin_bit_cast(V, pk),
+                                            reinterpret_cast<V*>(at(reinterpret_cast<P16*>(orow), lane,
+                                                                    (uint32_t)(g * PACK * I::NS * sizeof(O)))));
+#endif
+            }
+        }
+    }
+    template <int D, typename F> __device__ static __forceinline__ void xpose_any(F& a, F& b, bool hi) {
+        if constexpr (std::is_same<F, float>::value || std::is_same<F, double>::value) xpose2<D>(a, b, hi);
+        else xpose2(a, b, hi, D);
+    }
     template <int K>
     __device__ static __forceinline__ void one(const C2<T>* o, void* orow, int t) {
         constexpr int q = (K / R) * STEP, i = K % R;
@@ -426,8 +541,8 @@ struct LastStores {
 // queue drains continuously instead of in one burst that stalls every wave.
 constexpr int kChunks = 4;
 
-#ifndef NW_WMODE
-#define NW_WMODE 1      // 0: W in registers for the block; 1: W loaded in pass 0; 2: re-evaluated
+#ifndef NW_WREG_MAX_E
+#define NW_WREG_MAX_E 16   // W held in registers for the block when E <= this
 #endif
 #ifndef NW_XPREFETCH
 #define NW_XPREFETCH 0   // 1: next signal's X loaded into registers ahead of the stores (needs the
@@ -439,6 +554,25 @@ constexpr int kChunks = 4;
 
 // complex W rows (tables) keep the register path: with LDS-DMA they exceed 128 VGPRs
 template <typename T, int E, bool REALW> constexpr bool kXDMA = sizeof(T) == 4 && E >= NW_XDMA_MIN_E && REALW;
+
+// E = 16 (n <= 8192): X gets its OWN LDS buffer after the image and the pass-1 table, so
+// the next signal's X is DMA'd right after this signal's pass 0 and has the whole signal
+// (exchanges, passes, stores) to land; with W in registers, pass 0 then waits on nothing
+// issued after a store.  (At n = 16384 the 64 KiB buffer would cost a workgroup per CU.)
+#ifndef NW_XBUF
+#define NW_XBUF 0   // measured slower (C3 0.337 -> 0.360 ms): the buffer costs workgroups per CU
+#endif
+template <typename T, int N, int E> struct XBuf {
+    static constexpr bool ON = NW_XBUF && E < 32 && E <= NW_WREG_MAX_E;
+    static constexpr int OFFSET = lds_elems<N, E>() * (int)sizeof(T) + Tab1<T, N, E>::BYTES;
+    static constexpr int BYTES = ON ? (N / 2) * (int)sizeof(C2<T>) : 0;
+    static_assert(OFFSET % 16 == 0, "DMA alignment");
+    __device__ static __forceinline__ C2<T>* at_lds(T* lds) {
+        return reinterpret_cast<C2<T>*>(reinterpret_cast<char*>(lds) + OFFSET);
+    }
+};
+template <typename T, int N, int E> constexpr int kLdsBytes =
+    lds_elems<N, E>() * (int)sizeof(T) + Tab1<T, N, E>::BYTES + XBuf<T, N, E>::BYTES;
 
 template <typename T, int N, int E, int OUT, int C>
 __device__ __forceinline__ void drain(const C2<T>* o, void* oprev, int t) {
@@ -453,17 +587,25 @@ __device__ __forceinline__ void drain(const C2<T>* o, void* oprev, int t) {
 // next signal (drain) or by the caller after the last signal.
 template <typename T, int N, int E, int OUT, int P, bool XD>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>* __restrict__ tw, C2<T>* x,
-                                            const C2<T>* xs_next, bool interp, C2<T>* o, void* oprev, void* ocur,
+                                            const C2<T>* xs_next, C2<T>* o, void* oprev, void* ocur,
                                             Stamps* st) {
     using I = PassInfo<N, E, P>;
     if constexpr (P < Geometry<N, E>::npass()) {
         constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
+        constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;
         C2<T> pb[Q][LR > 0 ? LR : 1];
 #ifndef NW_ABL_NOTWIDDLE
+        if constexpr (!TABLED) {
 #pragma unroll
-        for (int q = 0; q < Q; ++q) twiddle_bases<T, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
+            for (int q = 0; q < Q; ++q) twiddle_bases<T, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
+        }
 #endif
+#ifndef NW_ABL_NOEXCH
         lds_barrier();                         // earlier readers of the image are done
+        if constexpr (P == 1 && XBuf<T, N, E>::ON) {
+            // every wave has read this signal's X: fetch the next one into the buffer
+            if (xs_next) dma_x<T, N, Geometry<N, E>::T>(xs_next, XBuf<T, N, E>::at_lds(lds), t);
+        }
         lds_write<T, N, E, P - 1, 0>(v, lds, t);
         lds_barrier();
         lds_read<T, N, E, P, 0>(v, lds, t);
@@ -471,10 +613,14 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
         lds_write<T, N, E, P - 1, 1>(v, lds, t);
         lds_barrier();
         lds_read<T, N, E, P, 1>(v, lds, t);
+#else   // ablation (diagnostic builds only): no exchange, the registers stay live
+#pragma unroll
+        for (int i = 0; i < E; ++i) asm volatile("" : "+v"(v[i].re), "+v"(v[i].im));
+#endif
         if constexpr (I::LAST && XD) {
             if (xs_next) {                     // the image is idle once every wave has read it
                 lds_barrier();
-                dma_x<N, Geometry<N, E>::T>(reinterpret_cast<const C2<float>*>(xs_next), lds, t);
+                dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -483,7 +629,16 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
 #ifndef NW_ABL_NOTWIDDLE
-            twiddle_apply<T, R>(v + q * R, pb[q]);
+            if constexpr (TABLED) {
+                const C2<T>* tab = Tab1<T, N, E>::table(lds) + I::bfly(t, q) % I::NS;
+#pragma unroll
+                for (int r = 1; r < R; ++r) {
+                    v[q * R + r] = cmul(v[q * R + r], tab[(r - 1) * I::NS]);
+                    if (r % 8 == 7) __builtin_amdgcn_sched_barrier(0);   // <= 8 twiddles in flight
+                }
+            } else {
+                twiddle_apply<T, R>(v + q * R, pb[q]);
+            }
 #endif
             idft_br<T, R>(v + q * R);
         }
@@ -495,27 +650,29 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
                 drain<T, N, E, OUT, 2 * P + 2>(o, oprev, t);
             }
 #if NW_XPREFETCH
-            if (xs_next) load_x<T, N, E>(x, xs_next, t, interp);
+            if (xs_next) load_x<T, N, E>(x, xs_next, t);
 #endif
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (NW_DEFER) {
 #pragma unroll
                 for (int k = 0; k < E; ++k) o[k] = v[k];
             } else {
-                LastStores<T, N, E, OUT>::template chunk<0, 1>(v, ocur, t);
+                LastStores<T, N, E, OUT>::all(v, ocur, t);
             }
         } else {
             drain<T, N, E, OUT, 2 * P>(o, oprev, t);
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, interp, o, oprev, ocur, st);
+            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, o, oprev, ocur, st);
         }
     }
 }
 
 // X[k] at the thread's pass-0 bins k = t + r*T from the R2C half spectrum xs.
 // k < N/2 exactly when r < E/2 (compile-time), so no branch: X[k], or conj(X[N - k])
-// above N/2 (at k = N/2 the bin is real).  interpolate_alias zeroes k >= int(N/2).
+// above N/2 (at k = N/2 the bin is real).  interpolate_alias (zero X[k], k >= int(N/2),
+// base.py:400-401) is folded into the W table (W[f, k] = 0 there): same product for
+// every finite X, and no per-element masking in the kernel.
 template <typename T, int N, int E>
-__device__ __forceinline__ void load_x(C2<T>* x, const C2<T>* xs, int t, bool interp) {
+__device__ __forceinline__ void load_x(C2<T>* x, const C2<T>* xs, int t) {
     constexpr int TT = N / E;
     const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(C2<T>);
 #pragma unroll
@@ -531,7 +688,6 @@ __device__ __forceinline__ void load_x(C2<T>* x, const C2<T>* xs, int t, bool in
             x[r].im = -x[r].im;
         }
 #endif
-        if (r >= E / 2 && interp) x[r] = C2<T>{T(0), T(0)};
     }
 }
 
@@ -596,24 +752,22 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
     const int64_t s_begin = (int64_t)sg * group;
     const int64_t s_end = min(nsig, s_begin + group);
-    // interpolate_alias zeroes X[k], k >= int(N/2); k = t + r*T >= N/2 exactly when r >= E/2
-    const bool interp = d.xlim < N;
 
-    // W[f, k] at the thread's bins (1/n folded in).  NW_WMODE 0: evaluated once per block
-    // into registers; 1: read per signal from the device-built table (L2-shared by the
-    // XCD tile); 2: re-evaluated per signal (no registers held across signals).
+    // W[f, k] at the thread's bins (1/n folded in), from the device-built table (L2-shared
+    // by the XCD tile).  E <= NW_WREG_MAX_E: held in registers for the whole block, loaded
+    // before any store is in flight; E = 32: re-read per signal (no VGPRs to spare).
     const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * N;
     const uint32_t wo = (uint32_t)t * (uint32_t)sizeof(WT);
-#if NW_WMODE == 0
-    WT w[E];
+    constexpr bool WREG = E <= NW_WREG_MAX_E;
+    WT w[WREG ? E : 1];
+    if constexpr (WREG) {
 #pragma unroll
-    for (int r = 0; r < E; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
-#define NW_W_AT(r) w[r]
-#elif NW_WMODE == 1
-#define NW_W_AT(r) (*at(wrow, wo, (uint32_t)((r) * G::T * sizeof(WT))))
-#else
-#define NW_W_AT(r) wsel<T, REALW>(wavelet_bin<T>(d, fi, t + (r) * G::T))
-#endif
+        for (int r = 0; r < E; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
+    }
+    auto w_at = [&](int r) -> WT {
+        if constexpr (WREG) return w[r];
+        else return *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
+    };
 
 #ifdef NW_STAMPS
     Stamps stamps{};
@@ -622,6 +776,7 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
 #else
     Stamps* st = nullptr;
 #endif
+    Tab1<T, N, E>::fill(lds, tw, t);   // read after the first exchange's barriers
     C2<T> x[E];
     C2<T> o[E];                    // outputs of the previous signal, stored during this one (NW_DEFER)
     void* oprev = nullptr;
@@ -629,22 +784,24 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     // XDMA: X[N/2] (the real Nyquist bin, outside the DMA'd half) of the signal being
     // transformed, carried one signal ahead in registers so its load never queues behind
     // a store and is never folded into a private/LDS pointer select
+    constexpr bool XB = XBuf<T, N, E>::ON;
     C2<T> nyq{T(0), T(0)};
-    if constexpr (XD) {
+    if constexpr (XD || XB) {
         nyq = reinterpret_cast<const C2<T>*>(X + s_begin * d.nh)[N / 2];
-        dma_x<N, G::T>(reinterpret_cast<const C2<float>*>(X + s_begin * d.nh), lds, t);
+        dma_x<T, N, G::T>(reinterpret_cast<const C2<T>*>(X + s_begin * d.nh),
+                          XD ? (void*)lds : (void*)XBuf<T, N, E>::at_lds(lds), t);
     } else {
 #if NW_XPREFETCH
-        load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s_begin * d.nh), t, interp);
+        load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s_begin * d.nh), t);
 #endif
     }
     for (int64_t s = s_begin; s < s_end; ++s) {
-        if constexpr (XD) {
+        if constexpr (XD || XB) {
             // this wave's DMA landed (only the stores issued after it may be pending),
-            // then every wave's: the whole X[0 .. N/2) is in the image
+            // then every wave's: the whole X[0 .. N/2) is in LDS
             if (s == s_begin) wait_vmcnt<0>(); else wait_vmcnt<LastStores<T, N, E, OUT>::COUNT>();
             lds_barrier();
-            const C2<T>* xl = reinterpret_cast<const C2<T>*>(lds);
+            const C2<T>* xl = XD ? reinterpret_cast<const C2<T>*>(lds) : XBuf<T, N, E>::at_lds(lds);
             // X[N - k] for r >= E/2 from ONE base (the lowest address, r = E-1) and positive
             // immediate offsets: DS offsets are unsigned, so N - t - r*T per r would hold E/2
             // address registers
@@ -658,24 +815,23 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
                     if (r == E / 2 && t == 0) x[r] = nyq;   // lvalue select (nyq -> scratch)
                     x[r].im = -x[r].im;
                 }
-                if (r >= E / 2 && interp) x[r] = C2<T>{T(0), T(0)};
             }
             if (s + 1 < s_end) nyq = reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh)[N / 2];
         } else {
 #if !NW_XPREFETCH
-            load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s * d.nh), t, interp);
+            load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s * d.nh), t);
 #endif
         }
         // pass 0 (Ns = 1): z = W * X at k = t + r*T, radix-E IDFT in registers
         C2<T> v[E];
 #pragma unroll
-        for (int r = 0; r < E; ++r) v[r] = WLoad<T, REALW>::apply(NW_W_AT(r), x[r]);
+        for (int r = 0; r < E; ++r) v[r] = WLoad<T, REALW>::apply(w_at(r), x[r]);
         idft_br<T, E>(v);
         drain<T, N, E, OUT, 0>(o, oprev, t);
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
         void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
-        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, interp, o, oprev, ocur, st);
+        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, o, oprev, ocur, st);
         oprev = ocur;
     }
     // the last signal's outputs
@@ -696,7 +852,8 @@ __global__ __launch_bounds__(256) void wtable_kernel(WDesc d, void* wtab) {
     const int fi = blockIdx.y;
     const int64_t k = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (k >= d.n) return;
-    const cplx<T> w = wavelet_bin<T>(d, fi, k);
+    cplx<T> w = wavelet_bin<T>(d, fi, k);
+    if (k >= d.xlim) w = cplx<T>{T(0), T(0)};   // interpolate_alias of X (base.py:400-401)
     if constexpr (REALW)
         reinterpret_cast<T*>(wtab)[(int64_t)fi * d.n + k] = w.re;
     else
@@ -756,7 +913,7 @@ template <typename T, int N, int E, bool REALW>
 hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
                     hipStream_t s) {
     constexpr int threads = N / E;
-    const size_t lds = (size_t)lds_elems<N, E>() * sizeof(T);
+    const size_t lds = (size_t)kLdsBytes<T, N, E>;
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
@@ -778,7 +935,7 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
 
 template <typename T, int N, int E, bool REALW>
 hipError_t prepare_one() {
-    const int lds = (int)(lds_elems<N, E>() * sizeof(T));
+    const int lds = kLdsBytes<T, N, E>;
     hipError_t e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e == hipSuccess)
