@@ -149,6 +149,31 @@ int nw_execute(nw_plan* plan, const void* x, int64_t nsig, void* out, int out_ki
 int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t nsig,
                      void* out, int out_kind);
 
+/* Baseline correction (base.py:18-68: class Baseline; baseline_of at 18-20) of a real
+ * array x[count] (dtype NW_F32 / NW_F64).  The reference slices AXIS 0: for an array
+ * whose rows hold row_len elements the baseline is rows [row0, row1) (already
+ * normalised like a Python slice), i.e. the contiguous elements [row0*row_len,
+ * row1*row_len).  basemean = its mean and std = its population std (np.std), both over
+ * all of its elements, are reduced on the device in fp64; then out[i] = op(x[i]) in the
+ * array's precision:
+ *   NW_BL_MEAN    x - basemean                 (base.py:53-54)
+ *   NW_BL_RATIO   x / basemean                 (56-57)
+ *   NW_BL_PERCENT (x - basemean) / basemean    (59-60)
+ *   NW_BL_LOG     log10(x / basemean)          (62-63)
+ *   NW_BL_ZSCORE  (x - basemean) / std         (65-66)
+ *   NW_BL_ZLOG    log10(x / basemean) / std    (68-69)
+ * mem = NW_MEM_HOST (synchronous) or NW_MEM_DEVICE (pointers on `device`, synchronous
+ * on the device's null stream).  stats (optional, host) receives {basemean, std}.
+ * An empty baseline gives NaN statistics, like numpy. */
+#define NW_BL_MEAN    0
+#define NW_BL_RATIO   1
+#define NW_BL_PERCENT 2
+#define NW_BL_LOG     3
+#define NW_BL_ZSCORE  4
+#define NW_BL_ZLOG    5
+int nw_baseline(int device, int dtype, const void* x, int64_t count, int64_t row_len, int64_t row0,
+                int64_t row1, int op, void* out, int mem, double* stats);
+
 int nw_plan_set_stream(nw_plan* plan, void* hip_stream);   /* NULL: the plan's own stream */
 int nw_plan_sync(nw_plan* plan);
 int nw_plan_stats(nw_plan* plan, nw_stats* stats);

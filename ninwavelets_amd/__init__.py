@@ -11,9 +11,10 @@ EpochsWavelet; plus the batched device engine (``Plan``).  Plotting and
 from .base import WaveletBase, WaveletMode, pad_to, interpolate_alias
 from .wavelets import Morse, MorseMNE, Morlet, Haar, MexicanHat, Shannon
 from .mneutils import EpochsWavelet
+from .baseline import Baseline, baseline_of
 from .engine import Plan, execute_multi
 from . import _lib
 
-__all__ = ['WaveletBase', 'WaveletMode', 'Morse', 'MorseMNE', 'Morlet', 'Haar', 'MexicanHat',
+__all__ = ['Baseline', 'baseline_of', 'WaveletBase', 'WaveletMode', 'Morse', 'MorseMNE', 'Morlet', 'Haar', 'MexicanHat',
            'Shannon', 'EpochsWavelet', 'Plan', 'execute_multi', 'pad_to', 'interpolate_alias']
 __version__ = '0.1.0'

@@ -34,6 +34,7 @@ NW_TIMING = 0x100
 NW_OUT_CWT, NW_OUT_ABS, NW_OUT_POWER = 0, 1, 2
 NW_OUT_POWER_MEAN, NW_OUT_ITC, NW_OUT_POWER_SUM, NW_OUT_PHASE_SUM = 3, 4, 5, 6
 NW_MEM_HOST, NW_MEM_DEVICE = 0, 1
+NW_BL = {'mean': 0, 'ratio': 1, 'percent': 2, 'log': 3, 'zscore': 4, 'zlog': 5}
 
 
 class nw_grid(ctypes.Structure):
@@ -69,6 +70,8 @@ SIGNATURES = [
     ('nw_plan_wavelet_rows', ctypes.c_int, [_P, _P]),
     ('nw_execute', ctypes.c_int, [_P, _P, _I64, _P, ctypes.c_int, ctypes.c_int]),
     ('nw_execute_multi', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),
+    ('nw_baseline', ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _I64, _I64, _I64, _I64, ctypes.c_int, _P,
+                                   ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     ('nw_plan_set_stream', ctypes.c_int, [_P, _P]),
     ('nw_plan_sync', ctypes.c_int, [_P]),
     ('nw_plan_stats', ctypes.c_int, [_P, ctypes.POINTER(nw_stats)]),

@@ -717,6 +717,50 @@ int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t n
     return NW_OK;
 }
 
+int nw_baseline(int device, int dtype, const void* x, int64_t count, int64_t row_len, int64_t row0, int64_t row1,
+                int op, void* out, int mem, double* stats) {
+    if (dtype != NW_F32 && dtype != NW_F64) return fail(NW_E_INVALID, "nw_baseline: dtype must be NW_F32 or NW_F64");
+    if (op < NW_BL_MEAN || op > NW_BL_ZLOG) return fail(NW_E_INVALID, "nw_baseline: unknown op");
+    if (mem != NW_MEM_HOST && mem != NW_MEM_DEVICE) return fail(NW_E_INVALID, "nw_baseline: bad mem");
+    if (count < 0 || row_len < 1 || row0 < 0 || row1 < row0 || row1 > count / row_len)
+        return fail(NW_E_INVALID, "nw_baseline: baseline rows out of range");
+    if (count > 0 && (!x || !out)) return fail(NW_E_INVALID, "nw_baseline: null array");
+    int ndev = 0;
+    NW_TRY(nw_device_count(&ndev));
+    if (device < 0 || device >= ndev) return fail(NW_E_INVALID, "nw_baseline: device out of range");
+    DeviceGuard guard(device);
+    const size_t esz = dtype == NW_F32 ? sizeof(float) : sizeof(double);
+    const size_t bytes = (size_t)count * esz;
+    void* dx = const_cast<void*>(x);
+    void* dout = out;
+    void* work = nullptr;
+    int rc = NW_OK;
+    auto hip = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == NW_OK) rc = fail(NW_E_HIP, std::string("nw_baseline: ") + what + ": " + hipGetErrorString(e));
+        return e == hipSuccess;
+    };
+    const bool host = mem == NW_MEM_HOST;
+    if (hip(hipMalloc(&work, nw::BL_WORK_DOUBLES * sizeof(double)), "hipMalloc") && host && bytes) {
+        dx = dout = nullptr;
+        if (hip(hipMalloc(&dx, bytes), "hipMalloc") && hip(hipMalloc(&dout, bytes), "hipMalloc"))
+            hip(hipMemcpy(dx, x, bytes, hipMemcpyHostToDevice), "H2D");
+    }
+    if (rc == NW_OK)
+        hip(nw::launch_baseline(dtype, dx, count, row0 * row_len, row1 * row_len, op, dout, (double*)work, nullptr),
+            "launch");
+    if (rc == NW_OK) hip(hipStreamSynchronize(nullptr), "sync");
+    if (rc == NW_OK && host && bytes) hip(hipMemcpy(out, dout, bytes, hipMemcpyDeviceToHost), "D2H");
+    if (rc == NW_OK && stats)
+        hip(hipMemcpy(stats, (double*)work + (nw::BL_WORK_DOUBLES - 2), 2 * sizeof(double), hipMemcpyDeviceToHost),
+            "D2H stats");
+    if (work) (void)hipFree(work);
+    if (host && bytes) {
+        if (dx) (void)hipFree(dx);
+        if (dout) (void)hipFree(dout);
+    }
+    return rc;
+}
+
 int nw_plan_set_stream(nw_plan* p, void* stream) {
     if (!p) return fail(NW_E_INVALID, "nw_plan_set_stream: null plan");
     p->stream = stream ? (hipStream_t)stream : p->own_stream;

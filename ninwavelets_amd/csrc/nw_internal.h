@@ -130,6 +130,9 @@ hipError_t launch_accumulate(int dtype, int src_kind, const void* src, double* a
                              hipStream_t s);
 hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, int64_t fn, int64_t nsig,
                            hipStream_t s);
+constexpr int BL_WORK_DOUBLES = 1024 + 2;   // k_bl_partial blocks + (mean, std)
+hipError_t launch_baseline(int dtype, const void* x, int64_t count, int64_t b0, int64_t b1, int op, void* out,
+                           double* work, hipStream_t s);
 // fused engine (nw_fused.hip)
 bool       fused_supported(int64_t n, int dtype);
 hipError_t fused_prepare(int64_t n, int dtype);

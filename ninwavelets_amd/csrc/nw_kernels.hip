@@ -3,6 +3,7 @@
 //   K2  epilogue           |Y| or |Y|^2                          (base.py:409-443)
 //   rows                   the cached wavelet rows themselves     (base.py:221-279)
 //   accumulate / finalize  epoch reductions power / ITC          (mneutils.py:42-71)
+//   baseline               Baseline correction                   (base.py:18-68)
 //
 // K1 is HBM-write bound (8 or 16 B per output point, X re-read from L2): each
 // block evaluates W for one scale f and a 256*V-bin tile ONCE into registers,
@@ -206,6 +207,102 @@ hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, in
     } else {
         if (itc) k_finalize<double, true><<<blocks, 256, 0, s>>>(acc, (double*)out, fn, d);
         else k_finalize<double, false><<<blocks, 256, 0, s>>>(acc, (double*)out, fn, d);
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Baseline correction (base.py:18-68).  The statistics of the slice x[b0, b1) -- one
+// scalar mean and population std over ALL its elements (baseline.mean(), np.std) -- are
+// reduced in fp64 in a fixed order: per-block partials over a grid-stride loop, then
+// one block over the partials (deterministic, run to run).  PASS 0 sums x, PASS 1 sums
+// (x - mean)^2 with the mean read back from stats[0].
+// ---------------------------------------------------------------------------
+constexpr int BL_THREADS = 256;
+constexpr int BL_BLOCKS = 1024;
+
+template <int PASS>
+__device__ __forceinline__ double block_sum(double v) {
+    __shared__ double sh[BL_THREADS];
+    sh[threadIdx.x] = v;
+    __syncthreads();
+    for (int w = BL_THREADS / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) sh[threadIdx.x] += sh[threadIdx.x + w];
+        __syncthreads();
+    }
+    return sh[0];
+}
+
+template <typename T, int PASS>
+__global__ __launch_bounds__(BL_THREADS) void k_bl_partial(const T* __restrict__ x, int64_t b0, int64_t b1,
+                                                           const double* __restrict__ stats,
+                                                           double* __restrict__ part) {
+    const double m = PASS == 1 ? stats[0] : 0.0;
+    double acc = 0.0;
+    for (int64_t i = b0 + (int64_t)blockIdx.x * BL_THREADS + threadIdx.x; i < b1; i += (int64_t)gridDim.x * BL_THREADS) {
+        const double v = (double)x[i];
+        acc += PASS == 0 ? v : (v - m) * (v - m);
+    }
+    const double tot = block_sum<PASS>(acc);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+// stats[PASS] = sum(part) / count  (PASS 1: sqrt -> population std); 0/0 = NaN for an
+// empty slice, as numpy's mean / std of nothing
+template <int PASS>
+__global__ __launch_bounds__(BL_THREADS) void k_bl_final(const double* __restrict__ part, int nparts, int64_t count,
+                                                         double* __restrict__ stats) {
+    double acc = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += BL_THREADS) acc += part[i];
+    const double tot = block_sum<PASS>(acc);
+    if (threadIdx.x == 0) {
+        const double q = tot / (double)count;
+        stats[PASS] = PASS == 0 ? q : sqrt(q);
+    }
+}
+
+// out = op(x) in the data's precision, with the statistics rounded to it (a float32 array
+// has float32 basemean / std in the reference, whose arithmetic order is kept:
+// base.py:53-68)
+template <typename T>
+__global__ __launch_bounds__(256) void k_bl_apply(const T* __restrict__ x, T* __restrict__ out, int64_t count,
+                                                  int op, const double* __restrict__ stats) {
+    const T m = (T)stats[0], sd = (T)stats[1];
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) {
+        const T v = x[i];
+        T r;
+        switch (op) {
+            case NW_BL_MEAN: r = v - m; break;
+            case NW_BL_RATIO: r = v / m; break;
+            case NW_BL_PERCENT: r = (v - m) / m; break;
+            case NW_BL_LOG: r = log10(v / m); break;
+            case NW_BL_ZSCORE: r = (v - m) / sd; break;
+            default: r = log10(v / m) / sd; break;      // NW_BL_ZLOG
+        }
+        out[i] = r;
+    }
+}
+
+hipError_t launch_baseline(int dtype, const void* x, int64_t count, int64_t b0, int64_t b1, int op, void* out,
+                           double* work /* BL_BLOCKS + 2 doubles */, hipStream_t s) {
+    double* part = work;
+    double* stats = work + BL_BLOCKS;
+    const int64_t n = std::max<int64_t>(0, b1 - b0);
+    const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(BL_BLOCKS, (n + BL_THREADS - 1) / BL_THREADS));
+    const int64_t ab = std::max<int64_t>(1, std::min<int64_t>((count + 255) / 256, 256 * 32));
+    if (dtype == NW_F32) {
+        k_bl_partial<float, 0><<<nb, BL_THREADS, 0, s>>>((const float*)x, b0, b1, stats, part);
+        k_bl_final<0><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
+        k_bl_partial<float, 1><<<nb, BL_THREADS, 0, s>>>((const float*)x, b0, b1, stats, part);
+        k_bl_final<1><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
+        if (count > 0) k_bl_apply<float><<<ab, 256, 0, s>>>((const float*)x, (float*)out, count, op, stats);
+    } else {
+        k_bl_partial<double, 0><<<nb, BL_THREADS, 0, s>>>((const double*)x, b0, b1, stats, part);
+        k_bl_final<0><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
+        k_bl_partial<double, 1><<<nb, BL_THREADS, 0, s>>>((const double*)x, b0, b1, stats, part);
+        k_bl_final<1><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
+        if (count > 0) k_bl_apply<double><<<ab, 256, 0, s>>>((const double*)x, (double*)out, count, op, stats);
     }
     return hipGetLastError();
 }

@@ -233,3 +233,25 @@ def make_example(length: float = 3.0) -> np.ndarray:
             + np.sin(np.pad(np.arange(0, length / 2, 0.001),
                             [int(length * 250), int(length * 250)], 'constant')
                      * 300 * 2 * np.pi))
+
+
+# ---------------------------------------------------------------------------
+# Baseline correction (base.py:18-68): slice AXIS 0, one scalar mean / population
+# std over the whole slice, then one elementwise op.
+# ---------------------------------------------------------------------------
+BASELINE_OPS = ('mean', 'ratio', 'percent', 'log', 'zscore', 'zlog')
+
+
+def baseline(wave: np.ndarray, sfreq: float, start: float, stop: float, op: str) -> np.ndarray:
+    """Baseline(wave, sfreq, start, stop).<op>() of base.py:23-68."""
+    part = wave[int(start * sfreq): int(stop * sfreq)]          # base.py:18-20, 49
+    m = part.mean()                                             # 50
+    ops = {
+        'mean': lambda: wave - m,                               # 53-54
+        'ratio': lambda: wave / m,                              # 56-57
+        'percent': lambda: (wave - m) / m,                      # 59-60
+        'log': lambda: np.log10(wave / m),                      # 62-63
+        'zscore': lambda: (wave - m) / np.std(part),            # 65-66
+        'zlog': lambda: np.log10(wave / m) / np.std(part),      # 68-69
+    }
+    return ops[op]()

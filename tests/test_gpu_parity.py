@@ -19,7 +19,7 @@ import ninwavelets_amd as nw  # noqa: E402
 
 TOL = {'float64': 1e-12, 'float32': 1e-5}
 ENGINES = ['rocfft', 'auto']
-SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs'))]
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline'))]
 CLASSES = {'morse': nw.Morse, 'morlet': nw.Morlet, 'shannon': nw.Shannon,
            'mexican_hat': nw.MexicanHat, 'haar': nw.Haar}
 
@@ -341,3 +341,38 @@ def test_c5_all_512_scales_into_hbm():
     torch.cuda.empty_cache()
     ref = O.cwt('morse', x.astype(np.float64), freqs[sel])
     assert rel_err(got, ref) <= 1e-4, rel_err(got, ref)
+
+
+
+# ------------------------------------------------------------------ Baseline (§8f rank 2)
+@pytest.mark.parametrize('name', golden_names('baseline'))
+def test_baseline_against_reference(name):
+    """nw_baseline (device fp64 statistics + elementwise op) against the reference's
+    Baseline outputs (base.py:18-68); axis 0 of an (F, N) power array is frequency.
+    Tolerance: 1e-13 relative (fp64), 2e-6 (fp32 data: numpy's float32 pairwise mean vs
+    the device's fp64 mean rounded to fp32)."""
+    g = load_golden(name)
+    m = g['meta']
+    t = 1e-13 if m['dtype'] == 'float64' else 2e-6
+    b = nw.Baseline(g['wave'], m['sfreq'], m['start'], m['stop'])
+    assert b.baseline.shape == g['baseline'].shape
+    assert abs(b.basemean - float(g['basemean'])) <= t * abs(float(g['basemean']))
+    for op in O.BASELINE_OPS:
+        got = getattr(b, op)()
+        assert got.dtype == g[op].dtype and got.shape == g[op].shape, op
+        assert rel_err(got, g[op]) <= t, (op, rel_err(got, g[op]))
+
+
+def test_baseline_device_tensor_and_edges():
+    torch = pytest.importorskip('torch')
+    rng = np.random.default_rng(3)
+    w = rng.uniform(0.5, 2.0, (64, 4096))
+    ref = O.baseline(w, 100., 0.1, 0.3, 'zlog')
+    wt = torch.from_numpy(w).cuda()
+    got = nw.Baseline(wt, 100., 0.1, 0.3).zlog()
+    assert got.is_cuda and rel_err(got.cpu().numpy(), ref) <= 1e-13
+    # negative start: a Python slice from the end, as in the reference
+    assert rel_err(nw.Baseline(w, 100., -0.2, 0.6).mean(), O.baseline(w, 100., -0.2, 0.6, 'mean')) <= 1e-13
+    # empty baseline: mean of nothing is NaN
+    with np.errstate(all='ignore'):
+        assert np.all(np.isnan(nw.Baseline(w, 100., 0.3, 0.1).ratio()))

@@ -7,7 +7,7 @@ import pytest
 from conftest import golden_names, load_golden
 from oracle import nw_oracle as O
 
-SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs'))]
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline'))]
 
 
 def _params(meta):
@@ -61,3 +61,14 @@ def test_oracle_reuse_quirk():
 def test_oracle_make_example_matches_fixture_input():
     g = load_golden('example_morse_power')
     np.testing.assert_array_equal(O.make_example(1.0), g['x'])
+
+
+@pytest.mark.parametrize('name', golden_names('baseline'))
+def test_oracle_baseline(name):
+    """Baseline correction (base.py:18-68) against the reference's own outputs."""
+    g = load_golden(name)
+    m = g['meta']
+    for op in O.BASELINE_OPS:
+        got = O.baseline(g['wave'], m['sfreq'], m['start'], m['stop'], op)
+        assert got.dtype == g[op].dtype
+        np.testing.assert_array_equal(got, g[op])
