@@ -47,6 +47,12 @@ extern "C" {
 #define NW_SHANNON 3   /* params: none (freq is ignored)    wavelets.py:256-262 */
 #define NW_TABLE   4   /* complex128 rows supplied by the host (WaveletMode.Normal,
                           user plugins overriding trans_formula/formula)          */
+#define NW_MEXICAN_HAT 5  /* params: sigma, sfreq, real_wave_length   wavelets.py:194-228 */
+#define NW_HAAR        6  /* params: sfreq, real_wave_length          wavelets.py:265-280
+                             Both are WaveletMode.Normal tables built ON THE DEVICE
+                             (base.py:249-256): the time-domain wavelet on np.arange's
+                             grid, zero-padded to ~sfreq*real_wave_length, fp64 rocFFT,
+                             |Re| + i|Im| (+ interpolate_alias), ragged row lengths. */
 
 /* plan flags */
 #define NW_INTERPOLATE   0x1u  /* zero the upper half of fft(x) (interpolate_alias, base.py:400-401) */
@@ -130,9 +136,14 @@ int nw_plan_set_wavelet(nw_plan* plan, int kind, const double* params, int npara
                         const double* freqs, const nw_grid* grid, const void* table,
                         const int64_t* row_len);
 
+/* Shape of the attached wavelet's cached rows: len_full (the table width; for the
+ * device-built NW_MEXICAN_HAT / NW_HAAR tables the longest row) and, if row_len is not
+ * NULL, each row's true length [nfreq] (ragged Normal-mode rows, base.py:253-254). */
+int nw_plan_wavelet_shape(nw_plan* plan, int64_t* len_full, int64_t* row_len);
+
 /* Evaluate the attached wavelet rows on the device and copy them to the host:
- * out[nfreq][grid.len_full] of the plan dtype (real for analytic kinds, complex
- * for NW_TABLE) -- the reference's self.fft_wavelets. */
+ * out[nfreq][len_full] of the plan dtype (real for analytic kinds, complex for the
+ * table kinds) -- the reference's self.fft_wavelets. */
 int nw_plan_wavelet_rows(nw_plan* plan, void* out_host);
 
 /* Run the CWT of nsig signals x[nsig][n] (plan dtype) into out[nsig][nfreq][n]

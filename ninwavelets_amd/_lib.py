@@ -27,6 +27,7 @@ NW_E_NODEVICE = -6
 
 NW_F32, NW_F64 = 0, 1
 NW_MORSE, NW_MORLET, NW_SHANNON, NW_TABLE = 1, 2, 3, 4
+NW_MEXICAN_HAT, NW_HAAR = 5, 6
 NW_INTERPOLATE = 0x1
 NW_ENGINE_ROCFFT = 0x10
 NW_ENGINE_FUSED = 0x20
@@ -67,6 +68,7 @@ SIGNATURES = [
     ('nw_plan_set_wavelet', ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
                                            ctypes.POINTER(ctypes.c_double), ctypes.POINTER(nw_grid), _P,
                                            ctypes.POINTER(ctypes.c_int64)]),
+    ('nw_plan_wavelet_shape', ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     ('nw_plan_wavelet_rows', ctypes.c_int, [_P, _P]),
     ('nw_execute', ctypes.c_int, [_P, _P, _I64, _P, ctypes.c_int, ctypes.c_int]),
     ('nw_execute_multi', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),

@@ -118,6 +118,11 @@ class WaveletBase:
         """(kind, params) when the stock analytic spectrum applies, else None."""
         return None
 
+    def _device_normal(self):
+        """(kind, params) when the stock time-domain formula applies (the table is then
+        built on the device), else None (plugin formulas: host-built table)."""
+        return None
+
     # ------------------------------------------------------------------ grids
     def _setup_trans_shape(self, freq: float, real_wave_length: float,
                            cuda: bool = False) -> np.ndarray:
@@ -178,6 +183,11 @@ class WaveletBase:
                 raise ZeroDivisionError
             kind, params = analytic
             cache = _Cache(kind, params, fr, L.trans_grid(real_length, self.sfreq, self.interpolate))
+        elif not spectral and self._device_normal() is not None:
+            if np.any(fr == 0):
+                raise ZeroDivisionError                  # make_wavelet, base.py:234-235
+            kind, params = self._device_normal()
+            cache = _Cache(kind, params, fr, L.nw_grid(1.0, 0, 0))
         else:
             rows = [self.make_fft_wavelet(f, real_length) for f in fr]
             if self.interpolate:
@@ -214,11 +224,14 @@ class WaveletBase:
             if c.kind == 'table':
                 self._rows = [row[:n] for row, n in zip(c.table, c.row_len)]
             else:
-                plan = Plan(max(1, c.grid.len_full), len(c.freqs), 'float64', self.device)
+                plan = Plan(max(1, c.grid.len_full), len(c.freqs), 'float64', self.device,
+                            interpolate=self.interpolate)   # Normal tables apply the alias mask
                 plan.set_wavelet(c.kind, c.params, c.freqs, c.grid)
                 rows = plan.rows()
+                lens = getattr(plan, 'row_len', None)
                 plan.close()
-                self._rows = [row for row in rows]
+                self._rows = ([row[:n] for row, n in zip(rows, lens)] if lens is not None
+                              else [row for row in rows])
         return self._rows
 
     @fft_wavelets.setter

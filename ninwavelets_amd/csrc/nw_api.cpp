@@ -92,6 +92,7 @@ struct nw_plan {
     float* d_xstep32 = nullptr;
     void* d_table = nullptr;
     int64_t* d_row_len = nullptr;
+    std::vector<int64_t> row_len_host;   // tables: true length of each row
 
     // buffers
     void* d_x = nullptr;
@@ -399,6 +400,13 @@ static int64_t arange_len(double stop, double step) {
     return (int64_t)std::ceil(q);
 }
 
+// np.arange(start, stop, step) length for start != 0
+static int64_t arange_len_from(double start, double stop, double step) {
+    const double q = (stop - start) / step;
+    if (!(q > 0.0)) return 0;
+    return (int64_t)std::ceil(q);
+}
+
 int nw_trans_grid(double real_length, double sfreq, int interpolate, nw_grid* g) {
     if (!g || !(real_length > 0.0) || !(sfreq > 0.0))
         return fail(NW_E_INVALID, "nw_trans_grid: need real_length > 0, sfreq > 0");
@@ -477,10 +485,112 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     return NW_OK;
 }
 
+// WaveletMode.Normal table on the device (MexicanHat / Haar; base.py:249-256).  The row
+// geometry mirrors numpy on the host: _setup_waveletshape's span and step
+// (base.py:196-216, real_length = 1, zero_mean), np.arange's length ceil((stop - start)
+// / step) and fill, half = int((sfreq * real_wave_length - m) / 2) zeros per side
+// (base.py:253-254).  Rows of equal length share one batched fp64 rocFFT.
+static int build_normal_table(nw_plan* p, int kind, const double* params, int nparams, const double* freqs,
+                              int64_t* lmax_out) {
+    const int F = p->nfreq;
+    const double sigma = kind == NW_MEXICAN_HAT ? (nparams > 0 ? params[0] : 7.0) : 0.0;
+    const int o = kind == NW_MEXICAN_HAT ? 1 : 0;
+    const double sfreq = nparams > o ? params[o] : 1000.0;
+    const double rwl = nparams > o + 1 ? params[o + 1] : 1.0;
+    const double peak = kind == NW_MEXICAN_HAT ? std::sqrt(6.0) / M_PI / M_PI : 1.0;   // wavelets.py:227-228
+    std::vector<nw::NormalRow> rows(F);
+    std::map<int64_t, std::vector<int>> by_len;
+    int64_t lmax = 0;
+    for (int f = 0; f < F; ++f) {
+        const double fr = freqs[f];
+        const double total = 1.0 / peak * fr * 2.0 * M_PI;
+        const double one = 1.0 / sfreq * 2.0 * M_PI * fr / peak;
+        const double t0 = -total / 2.0, stop = total / 2.0;
+        const int64_t m = arange_len_from(t0, stop, one);
+        const int64_t half = (int64_t)((sfreq * rwl - (double)m) / 2.0);
+        if (half < 0) return fail(NW_E_INVALID, "nw_plan_set_wavelet: negative padding (np.zeros of a negative size)");
+        nw::NormalRow r{};
+        r.m = m;
+        r.half = half;
+        r.len = m + 2 * half;
+        r.t0 = t0;
+        r.t1 = t0 + one;
+        r.delta = r.t1 - t0;
+        rows[f] = r;
+        by_len[r.len].push_back(f);
+        lmax = std::max(lmax, r.len);
+    }
+    int64_t off = 0;
+    for (auto& kv : by_len)
+        for (int f : kv.second) {
+            rows[f].off = off;
+            off += kv.first;
+        }
+    const size_t tbytes = (size_t)F * lmax * 2 * p->esz;
+    std::vector<int64_t> lens(F);
+    for (int f = 0; f < F; ++f) lens[f] = rows[f].len;
+    p->row_len_host = lens;
+    void* d_rows = nullptr;
+    void* d_buf = nullptr;
+    void* d_work = nullptr;
+    int rc = NW_OK;
+    auto hip = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == NW_OK) rc = fail(NW_E_HIP, std::string("normal table: ") + what + ": " + hipGetErrorString(e));
+        return rc == NW_OK;
+    };
+    if (hip(hipMalloc(&d_rows, F * sizeof(nw::NormalRow)), "hipMalloc") &&
+        hip(hipMalloc(&d_buf, (size_t)std::max<int64_t>(off, 1) * 2 * sizeof(double)), "hipMalloc") &&
+        hip(hipMalloc(&p->d_table, std::max<size_t>(tbytes, 16)), "hipMalloc") &&
+        hip(hipMalloc((void**)&p->d_row_len, F * sizeof(int64_t)), "hipMalloc") &&
+        hip(hipMemcpy(d_rows, rows.data(), F * sizeof(nw::NormalRow), hipMemcpyHostToDevice), "H2D") &&
+        hip(hipMemcpy(p->d_row_len, lens.data(), F * sizeof(int64_t), hipMemcpyHostToDevice), "H2D") &&
+        hip(nw::launch_normal_time((const nw::NormalRow*)d_rows, F, lmax, kind, sigma, d_buf, p->stream), "time rows")) {
+        for (auto& kv : by_len) {
+            if (kv.first == 0) continue;
+            rocfft_plan pl = nullptr;
+            size_t len = (size_t)kv.first, ws = 0;
+            if (rocfft_plan_create(&pl, rocfft_placement_inplace, rocfft_transform_type_complex_forward,
+                                   rocfft_precision_double, 1, &len, kv.second.size(), nullptr) != rocfft_status_success) {
+                rc = fail(NW_E_ROCFFT, "normal table: rocfft_plan_create");
+                break;
+            }
+            rocfft_plan_get_work_buffer_size(pl, &ws);
+            if (ws > 0 && !hip(hipMalloc(&d_work, ws), "hipMalloc")) {
+                rocfft_plan_destroy(pl);
+                break;
+            }
+            rocfft_execution_info_set_stream(p->info, p->stream);
+            if (ws) rocfft_execution_info_set_work_buffer(p->info, d_work, ws);
+            void* ib[1] = {(char*)d_buf + (size_t)rows[kv.second[0]].off * 2 * sizeof(double)};
+            const bool ok = rocfft_execute(pl, ib, nullptr, p->info) == rocfft_status_success;
+            hip(hipStreamSynchronize(p->stream), "sync");
+            if (p->work_bytes) rocfft_execution_info_set_work_buffer(p->info, p->work, p->work_bytes);
+            rocfft_plan_destroy(pl);
+            if (d_work) {
+                (void)hipFree(d_work);
+                d_work = nullptr;
+            }
+            if (!ok) {
+                rc = fail(NW_E_ROCFFT, "normal table: rocfft_execute");
+                break;
+            }
+        }
+        if (rc == NW_OK)
+            hip(nw::launch_normal_finish((const nw::NormalRow*)d_rows, F, lmax, (p->flags & NW_INTERPOLATE) != 0,
+                                         d_buf, p->dtype, p->d_table, p->stream), "finish");
+        if (rc == NW_OK) hip(hipStreamSynchronize(p->stream), "sync");
+    }
+    if (d_rows) (void)hipFree(d_rows);
+    if (d_buf) (void)hipFree(d_buf);
+    *lmax_out = lmax;
+    return rc;
+}
+
 int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams, const double* freqs,
                         const nw_grid* grid, const void* table, const int64_t* row_len) {
     if (!p || !freqs || !grid) return fail(NW_E_INVALID, "nw_plan_set_wavelet: null argument");
-    if (kind < NW_MORSE || kind > NW_TABLE) return fail(NW_E_INVALID, "nw_plan_set_wavelet: unknown kind");
+    if (kind < NW_MORSE || kind > NW_HAAR) return fail(NW_E_INVALID, "nw_plan_set_wavelet: unknown kind");
+    const bool normal = kind == NW_MEXICAN_HAT || kind == NW_HAAR;
     if (kind == NW_TABLE && !table) return fail(NW_E_INVALID, "nw_plan_set_wavelet: NW_TABLE needs a table");
     if (grid->len_full < 0 || grid->len_valid < 0 || grid->len_valid > grid->len_full)
         return fail(NW_E_INVALID, "nw_plan_set_wavelet: bad grid lengths");
@@ -533,7 +643,7 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
         NW_HIP(hipFree(p->d_row_len));
         p->d_row_len = nullptr;
     }
-    if (kind == NW_TABLE) {
+    if (kind == NW_TABLE && !normal) {
         std::vector<int64_t> rl(F, grid->len_full);
         if (row_len)
             for (int i = 0; i < F; ++i) {
@@ -543,8 +653,17 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
             }
         NW_HIP(hipMalloc((void**)&p->d_row_len, F * sizeof(int64_t)));
         NW_HIP(hipMemcpy(p->d_row_len, rl.data(), F * sizeof(int64_t), hipMemcpyHostToDevice));
+        p->row_len_host = rl;
     }
-    if (kind == NW_TABLE && grid->len_full > 0) {
+    if (normal) {
+        int64_t lmax = 0;
+        NW_TRY(build_normal_table(p, kind, params, nparams, freqs, &lmax));
+        kind = NW_TABLE;               // from here on a (device-built) table like any other
+        d.kind = NW_TABLE;
+        d.delta = 1.0;
+        d.len_full = d.len_valid = lmax;
+    }
+    if (kind == NW_TABLE && !normal && grid->len_full > 0) {
         const size_t cnt = (size_t)F * grid->len_full;
         const size_t bytes = cnt * 2 * p->esz;
         NW_HIP(hipMalloc(&p->d_table, bytes));
@@ -565,6 +684,16 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
     p->desc = d;
     p->has_wavelet = true;
     p->wtab_valid = false;
+    return NW_OK;
+}
+
+int nw_plan_wavelet_shape(nw_plan* p, int64_t* len_full, int64_t* row_len) {
+    if (!p || !len_full) return fail(NW_E_INVALID, "nw_plan_wavelet_shape: null argument");
+    if (!p->has_wavelet) return fail(NW_E_STATE, "nw_plan_wavelet_shape: no wavelet attached");
+    *len_full = p->desc.len_full;
+    if (row_len)
+        for (int f = 0; f < p->nfreq; ++f)
+            row_len[f] = (p->desc.kind == NW_TABLE && !p->row_len_host.empty()) ? p->row_len_host[f] : p->desc.len_full;
     return NW_OK;
 }
 

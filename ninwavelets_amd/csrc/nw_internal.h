@@ -130,6 +130,18 @@ hipError_t launch_accumulate(int dtype, int src_kind, const void* src, double* a
                              hipStream_t s);
 hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, int64_t fn, int64_t nsig,
                            hipStream_t s);
+// WaveletMode.Normal rows built on the device (base.py:249-256): one row per freq, laid
+// out in the FFT scratch grouped by row length (off), m timeline samples between
+// `half` zeros on each side (len = m + 2*half), np.arange's fill (t0, t1, delta).
+struct NormalRow {
+    int64_t off, m, half, len;
+    double t0, t1, delta;
+};
+hipError_t launch_normal_time(const NormalRow* rows, int nrows, int64_t lmax, int kind, double sigma, void* buf,
+                              hipStream_t s);
+hipError_t launch_normal_finish(const NormalRow* rows, int nrows, int64_t lmax, bool interp, const void* buf,
+                                int dtype, void* table, hipStream_t s);
+
 constexpr int BL_WORK_DOUBLES = 1024 + 2;   // k_bl_partial blocks + (mean, std)
 hipError_t launch_baseline(int dtype, const void* x, int64_t count, int64_t b0, int64_t b1, int op, void* out,
                            double* work, hipStream_t s);

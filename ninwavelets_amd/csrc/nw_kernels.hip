@@ -4,6 +4,7 @@
 //   rows                   the cached wavelet rows themselves     (base.py:221-279)
 //   accumulate / finalize  epoch reductions power / ITC          (mneutils.py:42-71)
 //   baseline               Baseline correction                   (base.py:18-68)
+//   normal_time / finish   MexicanHat / Haar rows on the device  (base.py:249-256)
 //
 // K1 is HBM-write bound (8 or 16 B per output point, X re-read from L2): each
 // block evaluates W for one scale f and a 256*V-bin tile ONCE into registers,
@@ -207,6 +208,72 @@ hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, in
     } else {
         if (itc) k_finalize<double, true><<<blocks, 256, 0, s>>>(acc, (double*)out, fn, d);
         else k_finalize<double, false><<<blocks, 256, 0, s>>>(acc, (double*)out, fn, d);
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// WaveletMode.Normal rows (base.py:249-256 with make_wavelet 346-359 and
+// _setup_waveletshape 196-216).  Row f of the FFT scratch: `half` zeros, the
+// time-domain wavelet at np.arange's points (t0, t1 = t0 + step, then t0 + i*delta
+// with delta = t1 - t0, exactly as numpy fills a float arange), `half` zeros.
+// Round-to-nearest intrinsics keep every product and sum unfused, as numpy's.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double mexican_hat_f(double tc, double sigma) {
+    // (1 - np.power(tc / sigma, 2)) * np.exp(-np.square(tc) / np.square(sigma) / 2)  (wavelets.py:219-221)
+    const double a = __ddiv_rn(tc, sigma);
+    const double e = exp(__ddiv_rn(__ddiv_rn(-__dmul_rn(tc, tc), __dmul_rn(sigma, sigma)), 2.0));
+    return __dmul_rn(__dsub_rn(1.0, __dmul_rn(a, a)), e);
+}
+__device__ __forceinline__ double haar_f(double tc) {          // wavelets.py:272-280
+    return (tc > 0.0 && tc <= 1.0) ? 1.0 : ((tc > -1.0 && tc <= 0.0) ? -1.0 : 0.0);
+}
+
+__global__ __launch_bounds__(256) void k_normal_time(const NormalRow* __restrict__ rows, int kind, double sigma,
+                                                     double2* __restrict__ buf) {
+    const NormalRow r = rows[blockIdx.x];
+    for (int64_t j = threadIdx.x; j < r.len; j += blockDim.x) {
+        const int64_t i = j - r.half;
+        double v = 0.0;
+        if (i >= 0 && i < r.m) {
+            const double t = i == 0 ? r.t0 : (i == 1 ? r.t1 : __dadd_rn(r.t0, __dmul_rn((double)i, r.delta)));
+            v = kind == NW_MEXICAN_HAT ? mexican_hat_f(t, sigma) : haar_f(t);
+        }
+        buf[r.off + j] = double2{v, 0.0};
+    }
+}
+
+hipError_t launch_normal_time(const NormalRow* rows, int nrows, int64_t, int kind, double sigma, void* buf,
+                              hipStream_t s) {
+    if (nrows > 0) k_normal_time<<<nrows, 256, 0, s>>>(rows, kind, sigma, (double2*)buf);
+    return hipGetLastError();
+}
+
+// table[f][j] = |Re| + i|Im| of the row's spectrum (base.py:255-256), zero past its
+// length and, when interpolating, from int(len/2) on (interpolate_alias, base.py:107-123)
+template <typename T>
+__global__ __launch_bounds__(256) void k_normal_finish(const NormalRow* __restrict__ rows, int64_t lmax, int interp,
+                                                       const double2* __restrict__ buf, cplx<T>* __restrict__ table) {
+    const NormalRow r = rows[blockIdx.x];
+    const int64_t keep = interp ? r.len / 2 : r.len;
+    cplx<T>* row = table + (int64_t)blockIdx.x * lmax;
+    for (int64_t j = threadIdx.x; j < lmax; j += blockDim.x) {
+        cplx<T> v{T(0), T(0)};
+        if (j < keep) {
+            const double2 z = buf[r.off + j];
+            v = cplx<T>{(T)fabs(z.x), (T)fabs(z.y)};
+        }
+        row[j] = v;
+    }
+}
+
+hipError_t launch_normal_finish(const NormalRow* rows, int nrows, int64_t lmax, bool interp, const void* buf,
+                                int dtype, void* table, hipStream_t s) {
+    if (nrows > 0) {
+        if (dtype == NW_F32)
+            k_normal_finish<float><<<nrows, 256, 0, s>>>(rows, lmax, interp, (const double2*)buf, (cplx<float>*)table);
+        else
+            k_normal_finish<double><<<nrows, 256, 0, s>>>(rows, lmax, interp, (const double2*)buf, (cplx<double>*)table);
     }
     return hipGetLastError();
 }

@@ -19,7 +19,10 @@ OUT_KINDS = {'cwt': L.NW_OUT_CWT, 'abs': L.NW_OUT_ABS, 'power': L.NW_OUT_POWER,
              'power_mean': L.NW_OUT_POWER_MEAN, 'itc': L.NW_OUT_ITC,
              'power_sum': L.NW_OUT_POWER_SUM, 'phase_sum': L.NW_OUT_PHASE_SUM}
 REDUCTIONS = ('power_mean', 'itc', 'power_sum', 'phase_sum')
-KINDS = {'morse': L.NW_MORSE, 'morlet': L.NW_MORLET, 'shannon': L.NW_SHANNON, 'table': L.NW_TABLE}
+KINDS = {'morse': L.NW_MORSE, 'morlet': L.NW_MORLET, 'shannon': L.NW_SHANNON, 'table': L.NW_TABLE,
+         # WaveletMode.Normal tables built on the device (base.py:249-256)
+         'mexican_hat': L.NW_MEXICAN_HAT, 'haar': L.NW_HAAR}
+TABLE_KINDS = ('table', 'mexican_hat', 'haar')
 
 
 def np_dtype(dtype) -> np.dtype:
@@ -87,11 +90,18 @@ class Plan:
             self._h, KINDS[kind], p.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), int(p.size),
             freqs.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.byref(grid), tab_ptr, rl_ptr))
         self.kind, self.grid = kind, grid
+        if kind in TABLE_KINDS:                      # the width the device settled on
+            lf = ctypes.c_int64()
+            lens = np.empty(self.nfreq, dtype=np.int64)
+            L.check(L.lib().nw_plan_wavelet_shape(self._h, ctypes.byref(lf),
+                                                  lens.ctypes.data_as(ctypes.POINTER(ctypes.c_int64))))
+            self.grid = L.nw_grid(1.0, lf.value, lf.value)
+            self.row_len = lens
         self.wavelet_token = token
 
     def rows(self) -> np.ndarray:
         """Device-evaluated cached wavelet rows (nfreq, len_full)."""
-        dt = self.dtype if self.kind != 'table' else out_dtype(self.dtype, 'cwt')
+        dt = self.dtype if self.kind not in TABLE_KINDS else out_dtype(self.dtype, 'cwt')
         out = np.empty((self.nfreq, self.grid.len_full), dtype=dt)
         L.check(L.lib().nw_plan_wavelet_rows(self._h, out.ctypes.data_as(ctypes.c_void_p)))
         return out

@@ -121,6 +121,12 @@ class MexicanHat(WaveletBase):
     def peak_freq(self, freq: float) -> float:
         return np.sqrt(6) / np.pi / np.pi
 
+    def _device_normal(self):
+        cls = type(self)
+        if cls.formula is MexicanHat.formula and cls.peak_freq is MexicanHat.peak_freq:
+            return 'mexican_hat', [float(self.sigma), float(self.sfreq), float(self.real_wave_length)]
+        return None
+
 
 class Haar(WaveletBase):
     """Haar wavelet, time-domain table path (wavelets.py:265-280)."""
@@ -136,6 +142,12 @@ class Haar(WaveletBase):
         out[(timeline > -1.) & (timeline <= 0.)] = -1.
         timeline[...] = out                      # in place, as the reference's loop
         return timeline
+
+    def _device_normal(self):
+        cls = type(self)
+        if cls.formula is Haar.formula and cls.peak_freq is WaveletBase.peak_freq:
+            return 'haar', [float(self.sfreq), float(self.real_wave_length)]
+        return None
 
 
 class MorseMNE(Morse):

@@ -376,3 +376,28 @@ def test_baseline_device_tensor_and_edges():
     # empty baseline: mean of nothing is NaN
     with np.errstate(all='ignore'):
         assert np.all(np.isnan(nw.Baseline(w, 100., 0.3, 0.1).ratio()))
+
+
+# ------------------------------------------------------------------ Normal-mode tables on device
+@pytest.mark.parametrize('interpolate', [False, True])
+@pytest.mark.parametrize('kind', ['mexican_hat', 'haar'])
+def test_device_normal_table_equals_host_table(kind, interpolate):
+    """MexicanHat / Haar rows built on the device (time rows + rocFFT + |Re|+i|Im|,
+    base.py:249-256) equal the host-built rows of a plugin subclass with the same
+    formula (ragged lengths included), and so do the CWTs through them."""
+    base = CLASSES[kind]
+
+    class HostBuilt(base):
+        def formula(self, tc, freq=1):
+            return base.formula(self, tc, freq)
+
+    freqs = np.array([0.5, 3., 7.5, 20., 47., 101.])
+    dev, host = base(1000, interpolate=interpolate), HostBuilt(1000, interpolate=interpolate)
+    assert dev._device_normal() is not None and host._device_normal() is None
+    rd = dev.make_fft_wavelets(freqs, 2.048)
+    rh = host.make_fft_wavelets(freqs, 2.048)
+    assert [r.shape for r in rd] == [r.shape for r in rh]
+    for a, b in zip(rd, rh):
+        assert np.max(np.abs(a - b)) <= 1e-13 * max(1.0, np.max(np.abs(b)))
+    x = synth(1, 2048, 17)[0].astype(np.float64)
+    assert rel_err(dev.cwt(x, freqs), host.cwt(x, freqs)) <= 1e-13
