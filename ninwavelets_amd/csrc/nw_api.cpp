@@ -113,6 +113,11 @@ struct nw_plan {
     void* work = nullptr;
     size_t work_bytes = 0;
 
+    // host-buffer output: two pinned staging pieces (the DMA of piece i overlaps the
+    // host copy of piece i-1 into the caller's pageable array)
+    void* pinned[2] = {nullptr, nullptr};
+    hipEvent_t pinned_ev[2] = {nullptr, nullptr};
+
     // timing
     std::vector<Pending> pending;
     std::vector<hipEvent_t> event_pool;
@@ -354,6 +359,55 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     return NW_OK;
 }
 
+// ---- host-buffer copy-out: pinned double-buffered pieces + a multi-threaded host copy
+constexpr size_t kPiece = size_t(64) << 20;
+#ifndef NW_COPY_THREADS
+#define NW_COPY_THREADS 8
+#endif
+
+void parallel_copy(char* dst, const char* src, size_t bytes) {
+    const size_t min_share = size_t(4) << 20;
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const size_t nth = std::min<size_t>(std::min<size_t>(NW_COPY_THREADS, hw), std::max<size_t>(1, bytes / min_share));
+    if (nth <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t share = (bytes + nth - 1) / nth;
+    std::vector<std::thread> th;
+    for (size_t i = 1; i < nth; ++i) {
+        const size_t off = i * share;
+        if (off >= bytes) break;
+        th.emplace_back([=] { std::memcpy(dst + off, src + off, std::min(share, bytes - off)); });
+    }
+    std::memcpy(dst, src, std::min(share, bytes));
+    for (auto& t : th) t.join();
+}
+
+int copy_out(nw_plan* p, char* dst, const char* src, size_t bytes) {
+    if (!p->pinned[0]) {
+        for (int i = 0; i < 2; ++i) {
+            NW_HIP(hipHostMalloc(&p->pinned[i], kPiece, hipHostMallocDefault));
+            NW_HIP(hipEventCreateWithFlags(&p->pinned_ev[i], hipEventDisableTiming));
+        }
+    }
+    const size_t npieces = (bytes + kPiece - 1) / kPiece;
+    for (size_t i = 0; i <= npieces; ++i) {
+        if (i < npieces) {
+            const size_t off = i * kPiece;
+            NW_HIP(hipMemcpyAsync(p->pinned[i & 1], src + off, std::min(kPiece, bytes - off), hipMemcpyDeviceToHost,
+                                  p->stream));
+            NW_HIP(hipEventRecord(p->pinned_ev[i & 1], p->stream));
+        }
+        if (i > 0) {                                  // piece i-1 landed: copy it out while piece i flies
+            const size_t k = i - 1, off = k * kPiece;
+            NW_HIP(hipEventSynchronize(p->pinned_ev[k & 1]));
+            parallel_copy(dst + off, (const char*)p->pinned[k & 1], std::min(kPiece, bytes - off));
+        }
+    }
+    return NW_OK;
+}
+
 void free_plan(nw_plan* p) {
     for (auto& kv : p->fwd) rocfft_plan_destroy(kv.second);
     for (auto& kv : p->inv) rocfft_plan_destroy(kv.second);
@@ -367,6 +421,10 @@ void free_plan(nw_plan* p) {
         (void)hipEventDestroy(pe.b);
     }
     for (auto e : p->event_pool) (void)hipEventDestroy(e);
+    for (int i = 0; i < 2; ++i) {
+        if (p->pinned[i]) (void)hipHostFree(p->pinned[i]);
+        if (p->pinned_ev[i]) (void)hipEventDestroy(p->pinned_ev[i]);
+    }
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;
 }
@@ -752,10 +810,7 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
             }));
             void* dst = (p->engine == NW_ENGINE_ROCFFT && out_kind == NW_OUT_CWT) ? p->d_Y : p->d_out;
             NW_TRY(run_chunk(p, p->d_x, c, dst, out_kind, true));
-            NW_TRY(staged(p, ST_COPY, [&] {
-                NW_HIP(hipMemcpyAsync(os, dst, (size_t)c * row_out, hipMemcpyDeviceToHost, p->stream));
-                return NW_OK;
-            }));
+            NW_TRY(staged(p, ST_COPY, [&] { return copy_out(p, os, (const char*)dst, (size_t)c * row_out); }));
             NW_HIP(hipStreamSynchronize(p->stream));
         } else {
             NW_TRY(run_chunk(p, xs, c, os, out_kind, true));

@@ -27,6 +27,15 @@ def main():
         el = (time.perf_counter() - t0) / reps
         res[kind] = {'s_per_call': el, 'points_per_s': S * n * F / el,
                      'GB_out_per_s': out.nbytes / el / 1e9}
+    # the same, writing into one reused (already faulted-in) output array
+    plan = w._plan(n, S, 0)
+    o = np.empty((S, F, n), dtype=np.complex64)
+    plan.execute(x, out=o, out_kind='cwt')
+    t0 = time.perf_counter()
+    for _ in range(3):
+        plan.execute(x, out=o, out_kind='cwt')
+    el = (time.perf_counter() - t0) / 3
+    res['cwt_reused_out'] = {'s_per_call': el, 'points_per_s': S * n * F / el, 'GB_out_per_s': o.nbytes / el / 1e9}
     print(json.dumps(res))
 
 
