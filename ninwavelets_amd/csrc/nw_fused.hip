@@ -32,6 +32,13 @@
 #define NW_PACK_MAX 2      // measured (n = 4096): pairs of 8-B outputs 0.413 -> 0.403 ms (cwt);
                            // quads of 4-B outputs 0.337 -> 0.360 ms (power): slower, so off
 #endif
+#ifndef NW_PRUNE
+#define NW_PRUNE 1         // pass 0 skips the elements beyond the W row's support
+#endif
+#ifndef NW_PRUNE_MIN
+#define NW_PRUNE_MIN 4     // smallest pass-0 variant (support rounded up to it; 1 and 2 add
+                           // code without a measurable gain)
+#endif
 #ifndef NW_XDMA_MIN_E
 #define NW_XDMA_MIN_E 32 // fp32 with E >= this: the next signal's X copied into the idle LDS
                          // image by LDS-DMA before the stores (measured: E=32 1.99 -> 1.94 ms,
@@ -112,33 +119,41 @@ template <int R> __host__ __device__ constexpr int bitrev(int i) {
     return r;
 }
 
-// radix-2 DIF butterflies of one stage (half size H), unrolled by template recursion
-template <typename T, int R, int H, int G, int K>
+// radix-2 DIF butterflies of one stage (half size H), unrolled by template recursion.
+// NZ: only the first NZ elements of every group of 2H are nonzero (pruned inputs): a
+// butterfly whose partner is zero is a copy plus a twiddle, one with both zero is skipped
+// (exact: u + 0 = u), and every group keeps a nonzero prefix of min(NZ, H) after the stage.
+template <typename T, int R, int H, int G, int K, int NZ>
 __device__ __forceinline__ void dif_bfly(C2<T>* a) {
     if constexpr (G < R) {
         if constexpr (K < H) {
-            const C2<T> u = a[G + K], w = a[G + K + H];
-            a[G + K] = {u.re + w.re, u.im + w.im};
-            a[G + K + H] = twc<T, K, 2 * H>(C2<T>{u.re - w.re, u.im - w.im});
-            dif_bfly<T, R, H, G, K + 1>(a);
+            if constexpr (K + H < NZ) {
+                const C2<T> u = a[G + K], w = a[G + K + H];
+                a[G + K] = {u.re + w.re, u.im + w.im};
+                a[G + K + H] = twc<T, K, 2 * H>(C2<T>{u.re - w.re, u.im - w.im});
+            } else if constexpr (K < NZ) {
+                a[G + K + H] = twc<T, K, 2 * H>(a[G + K]);
+            }
+            dif_bfly<T, R, H, G, K + 1, NZ>(a);
         } else {
-            dif_bfly<T, R, H, G + 2 * H, 0>(a);
+            dif_bfly<T, R, H, G + 2 * H, 0, NZ>(a);
         }
     }
 }
 
-template <typename T, int R, int H>
+template <typename T, int R, int H, int NZ>
 __device__ __forceinline__ void dif_stages(C2<T>* a) {
     if constexpr (H >= 1) {
-        dif_bfly<T, R, H, 0, 0>(a);
-        dif_stages<T, R, H / 2>(a);
+        dif_bfly<T, R, H, 0, 0, NZ>(a);
+        dif_stages<T, R, H / 2, (NZ < H ? NZ : H)>(a);
     }
 }
 
-// inverse DFT of R registers, natural-order input, bit-reversed output
-template <typename T, int R>
+// inverse DFT of R registers, natural-order input, bit-reversed output; inputs r >= NZ
+// are zero (their registers must hold zeros)
+template <typename T, int R, int NZ = R>
 __device__ __forceinline__ void idft_br(C2<T>* v) {
-    if constexpr (R > 1) dif_stages<T, R, R / 2>(v);
+    if constexpr (R > 1) dif_stages<T, R, R / 2, NZ>(v);
 }
 
 template <int R> constexpr int ilog2() { return R <= 1 ? 0 : 1 + ilog2<R / 2>(); }
@@ -416,7 +431,9 @@ template <typename T, int N, int TT>
 __device__ __forceinline__ void dma_x(const C2<T>* xs, void* dst, int t) {
     constexpr int CH = (N / 2) * (int)sizeof(C2<T>) / 16;   // 16-byte chunks
     static_assert(CH % TT == 0, "whole DMA rounds");
-    const int wave_base = (t & ~63) * 16;
+    // wave-uniform LDS destination base in an SGPR (M0 takes it directly; a VGPR copy
+    // per chunk would be hoisted out of the signal loop and spilled)
+    const int wave_base = __builtin_amdgcn_readfirstlane((t & ~63) * 16);
     const uint32_t lane_off = (uint32_t)t * 16u;
 #pragma unroll
     for (int i = 0; i < CH / TT; ++i) {
@@ -544,10 +561,6 @@ constexpr int kChunks = 4;
 #ifndef NW_WREG_MAX_E
 #define NW_WREG_MAX_E 16   // W held in registers for the block when E <= this
 #endif
-#ifndef NW_XPREFETCH
-#define NW_XPREFETCH 0   // 1: next signal's X loaded into registers ahead of the stores (needs the
-                         // 256-VGPR budget; with 2 blocks per CU the other block hides the wait)
-#endif
 #ifndef NW_DEFER
 #define NW_DEFER 0     // deferred/interleaved stores: measured no gain (the CU store path is the limit)
 #endif
@@ -649,9 +662,6 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
                 drain<T, N, E, OUT, 2 * P + 1>(o, oprev, t);
                 drain<T, N, E, OUT, 2 * P + 2>(o, oprev, t);
             }
-#if NW_XPREFETCH
-            if (xs_next) load_x<T, N, E>(x, xs_next, t);
-#endif
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (NW_DEFER) {
 #pragma unroll
@@ -671,12 +681,12 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
 // above N/2 (at k = N/2 the bin is real).  interpolate_alias (zero X[k], k >= int(N/2),
 // base.py:400-401) is folded into the W table (W[f, k] = 0 there): same product for
 // every finite X, and no per-element masking in the kernel.
-template <typename T, int N, int E>
+template <typename T, int N, int E, int NZ = E>
 __device__ __forceinline__ void load_x(C2<T>* x, const C2<T>* xs, int t) {
     constexpr int TT = N / E;
     const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(C2<T>);
 #pragma unroll
-    for (int r = 0; r < E; ++r) {
+    for (int r = 0; r < NZ; ++r) {
 #ifdef NW_ABL_NOXLOAD
         x[r] = {(T)(t + r), (T)r};
         asm volatile("" : "+v"(x[r].re), "+v"(x[r].im));
@@ -728,7 +738,7 @@ template <typename T, int N, int E, int OUT, bool REALW>
 __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
                                                             const void* __restrict__ wtab, void* __restrict__ out,
                                                             const C2<T>* __restrict__ tw, int64_t nsig, int group,
-                                                            int nsg_pad) {
+                                                            int nsg_pad, const int* __restrict__ wnz) {
     using G = Geometry<N, E>;
     using WT = typename WLoad<T, REALW>::type;
     constexpr bool XD = kXDMA<T, E, REALW>;
@@ -790,43 +800,59 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
         nyq = reinterpret_cast<const C2<T>*>(X + s_begin * d.nh)[N / 2];
         dma_x<T, N, G::T>(reinterpret_cast<const C2<T>*>(X + s_begin * d.nh),
                           XD ? (void*)lds : (void*)XBuf<T, N, E>::at_lds(lds), t);
-    } else {
-#if NW_XPREFETCH
-        load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s_begin * d.nh), t);
-#endif
     }
+    // W row support (device-built with the table): elements r >= nz of pass 0 multiply an
+    // exactly-zero W for every thread of the block (k = t + r*T beyond the row's last
+    // nonzero bin), so they are neither read nor multiplied and the DIF stages skip them
+    const int nz = NW_PRUNE ? wnz[fi] : E;
     for (int64_t s = s_begin; s < s_end; ++s) {
+        const C2<T>* xl = nullptr;
         if constexpr (XD || XB) {
             // this wave's DMA landed (only the stores issued after it may be pending),
             // then every wave's: the whole X[0 .. N/2) is in LDS
             if (s == s_begin) wait_vmcnt<0>(); else wait_vmcnt<LastStores<T, N, E, OUT>::COUNT>();
             lds_barrier();
-            const C2<T>* xl = XD ? reinterpret_cast<const C2<T>*>(lds) : XBuf<T, N, E>::at_lds(lds);
-            // X[N - k] for r >= E/2 from ONE base (the lowest address, r = E-1) and positive
-            // immediate offsets: DS offsets are unsigned, so N - t - r*T per r would hold E/2
-            // address registers
-            const C2<T>* xm = xl + (N - (E - 1) * G::T - t);
-#pragma unroll
-            for (int r = 0; r < E; ++r) {
-                if (r < E / 2) {
-                    x[r] = xl[t + r * G::T];
-                } else {                        // X[N - k]; k = N/2 (t = 0, r = E/2) is the Nyquist bin
-                    x[r] = xm[(E - 1 - r) * G::T];  // value copies: `c ? nyq : xl[m]` is an
-                    if (r == E / 2 && t == 0) x[r] = nyq;   // lvalue select (nyq -> scratch)
-                    x[r].im = -x[r].im;
-                }
-            }
-            if (s + 1 < s_end) nyq = reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh)[N / 2];
-        } else {
-#if !NW_XPREFETCH
-            load_x<T, N, E>(x, reinterpret_cast<const C2<T>*>(X + s * d.nh), t);
-#endif
+            xl = XD ? reinterpret_cast<const C2<T>*>(lds) : XBuf<T, N, E>::at_lds(lds);
         }
-        // pass 0 (Ns = 1): z = W * X at k = t + r*T, radix-E IDFT in registers
         C2<T> v[E];
+        // pass 0 (Ns = 1): z = W * X at k = t + r*T, r < NZ, radix-E IDFT in registers
+        auto pass0 = [&]<int NZ>() {
+            if constexpr (XD || XB) {
+                // the lane index made opaque HERE: LDS reads are speculatable, and hoisted
+                // above the variant dispatch they would all be live at once and spill
+                int tl = t;
+                asm volatile("" : "+v"(tl));
+                // X[N - k] for r >= E/2 from ONE base (the lowest address, r = E-1) and positive
+                // immediate offsets: DS offsets are unsigned, so N - t - r*T per r would hold
+                // E/2 address registers
+                const C2<T>* xm = xl + (N - (E - 1) * G::T - tl);
 #pragma unroll
-        for (int r = 0; r < E; ++r) v[r] = WLoad<T, REALW>::apply(w_at(r), x[r]);
-        idft_br<T, E>(v);
+                for (int r = 0; r < NZ; ++r) {
+                    if (r < E / 2) {
+                        x[r] = xl[tl + r * G::T];
+                    } else {                        // X[N - k]; k = N/2 (t = 0, r = E/2) is the Nyquist bin
+                        x[r] = xm[(E - 1 - r) * G::T];  // value copies: `c ? nyq : xl[m]` is an
+                        if (r == E / 2 && t == 0) x[r] = nyq;   // lvalue select (nyq -> scratch)
+                        x[r].im = -x[r].im;
+                    }
+                }
+            } else {
+                load_x<T, N, E, NZ>(x, reinterpret_cast<const C2<T>*>(X + s * d.nh), t);
+            }
+#pragma unroll
+            for (int r = 0; r < E; ++r)
+                v[r] = r < NZ ? WLoad<T, REALW>::apply(w_at(r), x[r]) : C2<T>{T(0), T(0)};
+            idft_br<T, E, NZ>(v);
+        };
+        if (NW_PRUNE_MIN <= 1 && nz <= 1) pass0.template operator()<1>();
+        else if (NW_PRUNE_MIN <= 2 && nz <= 2) pass0.template operator()<2>();
+        else if (nz <= 4) pass0.template operator()<4>();
+        else if (nz <= 8) pass0.template operator()<8>();
+        else if (E > 16 && nz <= 16) pass0.template operator()<(E > 16 ? 16 : E)>();
+        else pass0.template operator()<E>();
+        if constexpr (XD || XB) {
+            if (s + 1 < s_end) nyq = reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh)[N / 2];
+        }
         drain<T, N, E, OUT, 0>(o, oprev, t);
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
@@ -858,6 +884,37 @@ __global__ __launch_bounds__(256) void wtable_kernel(WDesc d, void* wtab) {
         reinterpret_cast<T*>(wtab)[(int64_t)fi * d.n + k] = w.re;
     else
         reinterpret_cast<C2<T>*>(wtab)[(int64_t)fi * d.n + k] = C2<T>{w.re, w.im};
+}
+
+// Support of each W row for pass-0 pruning: wnz[f] = the smallest power of two >= the
+// number of pass-0 elements r (bins k = t + r*T, t < T) reaching the row's last nonzero
+// bin, i.e. elements r >= wnz[f] see W = 0 exactly for every thread.
+template <typename T, bool REALW>
+__global__ __launch_bounds__(256) void wsupport_kernel(const void* wtab, int64_t n, int tt, int e, int* wnz) {
+    __shared__ int kmax[256];
+    const int fi = blockIdx.x;
+    int m = -1;
+    for (int64_t k = threadIdx.x; k < n; k += 256) {
+        bool nzv;
+        if constexpr (REALW) nzv = reinterpret_cast<const T*>(wtab)[(int64_t)fi * n + k] != T(0);
+        else {
+            const C2<T> w = reinterpret_cast<const C2<T>*>(wtab)[(int64_t)fi * n + k];
+            nzv = w.re != T(0) || w.im != T(0);
+        }
+        if (nzv) m = (int)k;
+    }
+    kmax[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) kmax[threadIdx.x] = max(kmax[threadIdx.x], kmax[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const int need = kmax[0] < 0 ? 1 : kmax[0] / tt + 1;   // elements 0 .. need-1 can be nonzero
+        int p2 = 1;
+        while (p2 < need) p2 <<= 1;
+        wnz[fi] = p2 < e ? p2 : e;
+    }
 }
 
 template <typename T>
@@ -909,6 +966,12 @@ hipError_t twiddles_for(int64_t n, int dtype, void** out) {
 }
 
 
+// bytes of the W rows in the table buffer (the wnz[nfreq] support array follows them)
+size_t wtab_row_bytes(int64_t n, int nfreq, size_t esz, bool realw) {
+    const size_t b = (size_t)n * nfreq * esz * (realw ? 1 : 2);
+    return (b + 15) / 16 * 16;
+}
+
 template <typename T, int N, int E, bool REALW>
 hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
                     hipStream_t s) {
@@ -924,12 +987,14 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
     const cplx<T>* Xc = reinterpret_cast<const cplx<T>*>(X);
     const C2<T>* twc_ = reinterpret_cast<const C2<T>*>(tw);
+    const int* wnz = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
+                                                  wtab_row_bytes(N, d.nfreq, sizeof(T), REALW));
     if (out_kind == NW_OUT_CWT)
-        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad);
+        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad, wnz);
     else if (out_kind == NW_OUT_POWER)
-        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad);
+        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad, wnz);
     else
-        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad);
+        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad, wnz);
     return hipGetLastError();
 }
 
@@ -984,18 +1049,31 @@ hipError_t fused_prepare(int64_t n, int dtype) {
 
 size_t fused_wtable_bytes(int64_t n, int nfreq, int dtype, int kind) {
     const size_t esz = dtype == NW_F32 ? sizeof(float) : sizeof(double);
-    return (size_t)n * nfreq * esz * (kind == NW_TABLE ? 2 : 1);
+    return wtab_row_bytes(n, nfreq, esz, kind != NW_TABLE) + (size_t)nfreq * sizeof(int);   // + wnz[nfreq]
 }
 
 hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
     dim3 grid((unsigned)((d.n + 255) / 256), (unsigned)d.nfreq);
     const bool realw = d.kind != NW_TABLE;
+    const size_t esz = dtype == NW_F32 ? sizeof(float) : sizeof(double);
+    int* wnz = reinterpret_cast<int*>(reinterpret_cast<char*>(wtab) + wtab_row_bytes(d.n, d.nfreq, esz, realw));
+    int e = 0;
+#define NW_E_OF(TY, NN, EE) \
+    if (d.n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) e = EE;
+    NW_FUSED_TABLE(NW_E_OF)
+#undef NW_E_OF
+    if (e == 0) return hipErrorNotSupported;
+    const int tt = (int)(d.n / e);
     if (dtype == NW_F32) {
         if (realw) wtable_kernel<float, true><<<grid, 256, 0, s>>>(d, wtab);
         else wtable_kernel<float, false><<<grid, 256, 0, s>>>(d, wtab);
+        if (realw) wsupport_kernel<float, true><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
+        else wsupport_kernel<float, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
     } else {
         if (realw) wtable_kernel<double, true><<<grid, 256, 0, s>>>(d, wtab);
         else wtable_kernel<double, false><<<grid, 256, 0, s>>>(d, wtab);
+        if (realw) wsupport_kernel<double, true><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
+        else wsupport_kernel<double, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
     }
     return hipGetLastError();
 }
