@@ -553,16 +553,9 @@ struct LastStores {
     }
 };
 
-// Store chunks of the PREVIOUS signal are interleaved with this signal's phases
-// (kChunks points: after pass 0, then around every exchange), so the CU's store
-// queue drains continuously instead of in one burst that stalls every wave.
-constexpr int kChunks = 4;
 
 #ifndef NW_WREG_MAX_E
 #define NW_WREG_MAX_E 16   // W held in registers for the block when E <= this
-#endif
-#ifndef NW_DEFER
-#define NW_DEFER 0     // deferred/interleaved stores: measured no gain (the CU store path is the limit)
 #endif
 
 // complex W rows (tables) keep the register path: with LDS-DMA they exceed 128 VGPRs
@@ -587,20 +580,15 @@ template <typename T, int N, int E> struct XBuf {
 template <typename T, int N, int E> constexpr int kLdsBytes =
     lds_elems<N, E>() * (int)sizeof(T) + Tab1<T, N, E>::BYTES + XBuf<T, N, E>::BYTES;
 
-template <typename T, int N, int E, int OUT, int C>
-__device__ __forceinline__ void drain(const C2<T>* o, void* oprev, int t) {
-    if constexpr (NW_DEFER && C < kChunks)
-        if (oprev) LastStores<T, N, E, OUT>::template chunk<C, kChunks>(o, oprev, t);
-}
 
 // ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P.
-// In the last pass the NEXT signal's X is loaded (into x) before anything else is
-// issued: loads and stores retire in one in-order vmcnt queue, so the next pass 0
-// waits for its loads only.  The outputs are moved to o and stored during the
-// next signal (drain) or by the caller after the last signal.
+// In the last pass (LDS-DMA kernels) the NEXT signal's X is DMA'd into the idle image
+// before this signal's stores are issued: loads, stores and LDS-DMA retire in one
+// in-order vmcnt queue, so the next pass 0 waits for that DMA only.  The last pass
+// stores its outputs straight to HBM.
 template <typename T, int N, int E, int OUT, int P, bool XD>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>* __restrict__ tw, C2<T>* x,
-                                            const C2<T>* xs_next, C2<T>* o, void* oprev, void* ocur,
+                                            const C2<T>* xs_next, void* ocur,
                                             Stamps* st) {
     using I = PassInfo<N, E, P>;
     if constexpr (P < Geometry<N, E>::npass()) {
@@ -637,7 +625,6 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
-        drain<T, N, E, OUT, 2 * P - 1>(o, oprev, t);
         NW_STAMP(st, 2 * P - 1);               // exchange P-1 -> P
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
@@ -657,21 +644,10 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
         }
         NW_STAMP(st, 2 * P);                   // pass P arithmetic
         if constexpr (I::LAST) {
-            drain<T, N, E, OUT, 2 * P>(o, oprev, t);        // anything left of the previous signal
-            if constexpr (2 * P < kChunks - 1) {
-                drain<T, N, E, OUT, 2 * P + 1>(o, oprev, t);
-                drain<T, N, E, OUT, 2 * P + 2>(o, oprev, t);
-            }
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (NW_DEFER) {
-#pragma unroll
-                for (int k = 0; k < E; ++k) o[k] = v[k];
-            } else {
-                LastStores<T, N, E, OUT>::all(v, ocur, t);
-            }
+            LastStores<T, N, E, OUT>::all(v, ocur, t);
         } else {
-            drain<T, N, E, OUT, 2 * P>(o, oprev, t);
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, o, oprev, ocur, st);
+            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st);
         }
     }
 }
@@ -788,8 +764,6 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
 #endif
     Tab1<T, N, E>::fill(lds, tw, t);   // read after the first exchange's barriers
     C2<T> x[E];
-    C2<T> o[E];                    // outputs of the previous signal, stored during this one (NW_DEFER)
-    void* oprev = nullptr;
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T));
     // XDMA: X[N/2] (the real Nyquist bin, outside the DMA'd half) of the signal being
     // transformed, carried one signal ahead in registers so its load never queues behind
@@ -853,15 +827,12 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
         if constexpr (XD || XB) {
             if (s + 1 < s_end) nyq = reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh)[N / 2];
         }
-        drain<T, N, E, OUT, 0>(o, oprev, t);
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
         void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
-        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, o, oprev, ocur, st);
-        oprev = ocur;
+        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, ocur, st);
     }
     // the last signal's outputs
-    if constexpr (NW_DEFER) LastStores<T, N, E, OUT>::template chunk<0, 1>(o, oprev, t);
     NW_STAMP(st, kStampsStore);
 #ifdef NW_STAMPS
     if ((t & 63) == 0) {
