@@ -185,6 +185,17 @@ int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t n
 int nw_baseline(int device, int dtype, const void* x, int64_t count, int64_t row_len, int64_t row0,
                 int64_t row1, int op, void* out, int mem, double* stats);
 
+/* Time-domain wavelets of the stock kinds, make_wavelet(s) (base.py:346-376), computed on
+ * `device`: one row per freq, complex128, left-aligned in out[nfreq][*max_len] (host).
+ *   NW_MORSE {b, r}, NW_SHANNON {}  (WaveletMode.Reverse): ifft of the spectrum (its
+ *     default freq = 1) on np.arange(0, sfreq/f*real_wave_length, 1/f), then the centre
+ *     slice [m//2, m//2*3) of hstack(conj(flip(w)), w)  -> 2*(m//2) points;
+ *   NW_MORLET {sigma, gabor[, c, k]}, NW_MEXICAN_HAT {sigma}, NW_HAAR {}: the time-domain
+ *     formula on np.arange(-T/2, T/2, step) of _setup_waveletshape (base.py:196-216).
+ * row_len[nfreq] receives each row's length.  out == NULL: lengths only (to size out). */
+int nw_make_wavelets(int device, int kind, const double* params, int nparams, const double* freqs, int nfreq,
+                     double sfreq, double real_wave_length, void* out, int64_t* max_len, int64_t* row_len);
+
 int nw_plan_set_stream(nw_plan* plan, void* hip_stream);   /* NULL: the plan's own stream */
 int nw_plan_sync(nw_plan* plan);
 int nw_plan_stats(nw_plan* plan, nw_stats* stats);

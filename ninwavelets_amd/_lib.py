@@ -74,6 +74,10 @@ SIGNATURES = [
     ('nw_execute_multi', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),
     ('nw_baseline', ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _I64, _I64, _I64, _I64, ctypes.c_int, _P,
                                    ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
+    ('nw_make_wavelets', ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_double,
+                                        ctypes.c_double, _P, ctypes.POINTER(ctypes.c_int64),
+                                        ctypes.POINTER(ctypes.c_int64)]),
     ('nw_plan_set_stream', ctypes.c_int, [_P, _P]),
     ('nw_plan_sync', ctypes.c_int, [_P]),
     ('nw_plan_stats', ctypes.c_int, [_P, ctypes.POINTER(nw_stats)]),

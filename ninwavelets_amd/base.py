@@ -26,6 +26,7 @@ from scipy.fftpack import fft, ifft
 
 from . import _lib as L
 from .engine import REDUCTIONS, Plan, execute_multi, np_dtype
+from .engine import make_wavelets as _make_wavelets_dev
 
 # Device working-set budget per plan chunk (bytes); signals are streamed through it.
 CHUNK_BYTES = int(os.environ.get('NINWAVE_CHUNK_BYTES', str(4 << 30)))
@@ -138,10 +139,29 @@ class WaveletBase:
         return np.arange(-span / 2, span / 2, step) if zero_mean else np.arange(0, span, step)
 
     # ------------------------------------------------------------------ wavelets
+    def _time_formula_spec(self):
+        """(kind, params) when the stock time-domain formula applies (override)."""
+        return None
+
+    def _device_wavelet_spec(self):
+        """(kind, params) of nw_make_wavelets for this wavelet, None for plugin formulas."""
+        if self.mode in (WaveletMode.Reverse, WaveletMode.Twice):
+            a = self._analytic()
+            return a if a is not None and a[0] in ('morse', 'shannon') else None
+        return self._time_formula_spec()
+
+    def _device_wavelets(self, spec, freqs) -> list:
+        kind, params = spec
+        rows = _make_wavelets_dev(kind, params, freqs, self.sfreq, self.real_wave_length, self.device)
+        return [r.real.copy() for r in rows] if kind in ('mexican_hat', 'haar') else rows
+
     def make_wavelet(self, freq: float) -> np.ndarray:
-        """Time-domain wavelet (base.py:346-359)."""
+        """Time-domain wavelet (base.py:346-359): on the device for the stock wavelets."""
         if freq == 0:
             raise ZeroDivisionError
+        spec = self._device_wavelet_spec()
+        if spec is not None:
+            return self._device_wavelets(spec, [freq])[0]
         if self.mode in (WaveletMode.Reverse, WaveletMode.Twice):
             w = ifft(self.trans_formula(self._setup_trans_shape(freq, self.real_wave_length)))
             half = int(w.shape[0])
@@ -150,8 +170,16 @@ class WaveletBase:
         return self.formula(self._setup_waveletshape(freq, 1, zero_mean=True), freq)
 
     def make_wavelets(self, freqs) -> list:
-        """List of time-domain wavelets (base.py:361-376)."""
-        self.wavelets = [self.make_wavelet(f) for f in freqs]
+        """List of time-domain wavelets (base.py:361-376): one device call for the stock
+        wavelets (nw_make_wavelets), the plugin's own formula otherwise."""
+        spec = self._device_wavelet_spec()
+        if spec is not None:
+            fr = list(freqs)
+            if any(f == 0 for f in fr):
+                raise ZeroDivisionError
+            self.wavelets = self._device_wavelets(spec, fr)
+        else:
+            self.wavelets = [self.make_wavelet(f) for f in freqs]
         return self.wavelets
 
     def _normal_row(self, freq: float) -> np.ndarray:

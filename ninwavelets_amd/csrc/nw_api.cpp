@@ -945,6 +945,122 @@ int nw_baseline(int device, int dtype, const void* x, int64_t count, int64_t row
     return rc;
 }
 
+int nw_make_wavelets(int device, int kind, const double* params, int nparams, const double* freqs, int nfreq,
+                     double sfreq, double rwl, void* out, int64_t* max_len, int64_t* row_len) {
+    const bool reverse = kind == NW_MORSE || kind == NW_SHANNON;
+    if (!reverse && kind != NW_MORLET && kind != NW_MEXICAN_HAT && kind != NW_HAAR)
+        return fail(NW_E_INVALID, "nw_make_wavelets: kind must be a stock wavelet");
+    if (nfreq < 0 || (nfreq > 0 && !freqs) || !max_len || !row_len) return fail(NW_E_INVALID, "nw_make_wavelets: null argument");
+    if (!(sfreq > 0.0)) return fail(NW_E_INVALID, "nw_make_wavelets: sfreq must be > 0");
+    nw::WaveParams wp{};
+    wp.kind = kind;
+    if (kind == NW_MORSE) {
+        wp.b = nparams > 0 ? params[0] : 17.5;
+        wp.r = nparams > 1 ? params[1] : 3.0;
+        wp.b_over_r = wp.b / wp.r;
+    } else if (kind == NW_MORLET) {
+        wp.sigma = nparams > 0 ? params[0] : 7.0;
+        const bool gabor = nparams > 1 && params[1] != 0.0;
+        const double s2 = wp.sigma * wp.sigma;
+        const double c = nparams > 2 ? params[2] : std::pow(1.0 + std::exp(-s2) - 2.0 * std::exp(-3.0 / 4.0 * s2), -0.5);
+        wp.cpi = c * std::pow(M_PI, -0.25);
+        wp.kappa = nparams > 3 ? params[3] : (gabor ? 0.0 : std::exp(-std::pow(wp.sigma, 2.0) / 2.0));
+    } else if (kind == NW_MEXICAN_HAT) {
+        wp.sigma = nparams > 0 ? params[0] : 7.0;
+    }
+    std::vector<nw::WaveRow> rows(nfreq);
+    std::map<int64_t, std::vector<int>> by_m;
+    int64_t lmax = 0, off = 0;
+    for (int f = 0; f < nfreq; ++f) {
+        const double fr = freqs[f];
+        if (fr == 0.0) return fail(NW_E_INVALID, "nw_make_wavelets: freq == 0 (ZeroDivisionError, base.py:347-348)");
+        nw::WaveRow r{};
+        if (reverse) {                        // _setup_trans_shape(freq, real_wave_length), base.py:191-194
+            const double one = 1.0 / fr;
+            r.m = arange_len(sfreq / fr * rwl, one);
+            r.len = 2 * (r.m / 2);
+            r.t0 = 0.0;
+            r.delta = one;
+            r.t1 = one;
+            by_m[r.m].push_back(f);
+        } else {                              // _setup_waveletshape(freq, 1, zero_mean=True), base.py:211-216
+            const double peak = kind == NW_MORLET ? wp.sigma / (1.0 - std::exp(-wp.sigma * fr))
+                                : kind == NW_MEXICAN_HAT ? std::sqrt(6.0) / M_PI / M_PI : 1.0;
+            const double total = 1.0 / peak * fr * 2.0 * M_PI;
+            const double one = 1.0 / sfreq * 2.0 * M_PI * fr / peak;
+            r.t0 = -total / 2.0;
+            r.m = arange_len_from(r.t0, total / 2.0, one);
+            r.len = r.m;
+            r.t1 = r.t0 + one;
+            r.delta = r.t1 - r.t0;
+        }
+        row_len[f] = r.len;
+        lmax = std::max(lmax, r.len);
+        rows[f] = r;
+    }
+    for (auto& kv : by_m)
+        for (int f : kv.second) {
+            rows[f].off = off;
+            off += kv.first;
+        }
+    *max_len = lmax;
+    if (!out || nfreq == 0 || lmax == 0) {
+        if (out && nfreq > 0) std::memset(out, 0, (size_t)nfreq * lmax * 16);
+        return NW_OK;
+    }
+    int ndev = 0;
+    NW_TRY(nw_device_count(&ndev));
+    if (device < 0 || device >= ndev) return fail(NW_E_INVALID, "nw_make_wavelets: device out of range");
+    std::call_once(g_rocfft_once, [] { rocfft_setup(); });
+    DeviceGuard guard(device);
+    void *d_rows = nullptr, *d_buf = nullptr, *d_out = nullptr, *d_work = nullptr;
+    rocfft_execution_info info = nullptr;
+    int rc = NW_OK;
+    auto hip = [&](hipError_t e, const char* what) {
+        if (e != hipSuccess && rc == NW_OK) rc = fail(NW_E_HIP, std::string("nw_make_wavelets: ") + what + ": " + hipGetErrorString(e));
+        return rc == NW_OK;
+    };
+    const size_t obytes = (size_t)nfreq * lmax * 16;
+    if (hip(hipMalloc(&d_rows, nfreq * sizeof(nw::WaveRow)), "hipMalloc") &&
+        hip(hipMalloc(&d_out, obytes), "hipMalloc") &&
+        hip(hipMemcpy(d_rows, rows.data(), nfreq * sizeof(nw::WaveRow), hipMemcpyHostToDevice), "H2D")) {
+        if (!reverse) {
+            hip(nw::launch_wavelet_time((const nw::WaveRow*)d_rows, nfreq, lmax, wp, d_out, nullptr), "time rows");
+        } else if (hip(hipMalloc(&d_buf, (size_t)std::max<int64_t>(off, 1) * 16), "hipMalloc") &&
+                   hip(nw::launch_wavelet_spectra((const nw::WaveRow*)d_rows, nfreq, wp, d_buf, nullptr), "spectra")) {
+            if (rocfft_execution_info_create(&info) != rocfft_status_success) rc = fail(NW_E_ROCFFT, "nw_make_wavelets: rocfft info");
+            for (auto& kv : by_m) {
+                if (rc != NW_OK || kv.first == 0) continue;
+                rocfft_plan pl = nullptr;
+                size_t len = (size_t)kv.first, ws = 0;
+                if (rocfft_plan_create(&pl, rocfft_placement_inplace, rocfft_transform_type_complex_inverse,
+                                       rocfft_precision_double, 1, &len, kv.second.size(), nullptr) != rocfft_status_success) {
+                    rc = fail(NW_E_ROCFFT, "nw_make_wavelets: rocfft_plan_create");
+                    break;
+                }
+                rocfft_plan_get_work_buffer_size(pl, &ws);
+                if (ws && hip(hipMalloc(&d_work, ws), "hipMalloc")) rocfft_execution_info_set_work_buffer(info, d_work, ws);
+                void* ib[1] = {(char*)d_buf + (size_t)rows[kv.second[0]].off * 16};
+                if (rc == NW_OK && rocfft_execute(pl, ib, nullptr, info) != rocfft_status_success)
+                    rc = fail(NW_E_ROCFFT, "nw_make_wavelets: rocfft_execute");
+                hip(hipDeviceSynchronize(), "sync");
+                rocfft_plan_destroy(pl);
+                if (d_work) {
+                    (void)hipFree(d_work);
+                    d_work = nullptr;
+                }
+            }
+            if (rc == NW_OK) hip(nw::launch_wavelet_pack((const nw::WaveRow*)d_rows, nfreq, lmax, d_buf, d_out, nullptr), "pack");
+        }
+        if (rc == NW_OK) hip(hipDeviceSynchronize(), "sync");
+        if (rc == NW_OK) hip(hipMemcpy(out, d_out, obytes, hipMemcpyDeviceToHost), "D2H");
+    }
+    if (info) rocfft_execution_info_destroy(info);
+    for (void* b : {d_rows, d_buf, d_out})
+        if (b) (void)hipFree(b);
+    return rc;
+}
+
 int nw_plan_set_stream(nw_plan* p, void* stream) {
     if (!p) return fail(NW_E_INVALID, "nw_plan_set_stream: null plan");
     p->stream = stream ? (hipStream_t)stream : p->own_stream;

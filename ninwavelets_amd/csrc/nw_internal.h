@@ -142,6 +142,24 @@ hipError_t launch_normal_time(const NormalRow* rows, int nrows, int64_t lmax, in
 hipError_t launch_normal_finish(const NormalRow* rows, int nrows, int64_t lmax, bool interp, const void* buf,
                                 int dtype, void* table, hipStream_t s);
 
+// Time-domain wavelets (base.py:346-376): Reverse kinds fill an fp64 spectrum row on
+// arange(0, sfreq/f*rwl, 1/f) (buffer offset `off`, m points), the time kinds a timeline
+// t0, t1, t0 + i*delta (m points); `len` is the returned row length.
+struct WaveRow {
+    int64_t off, m, len;
+    double t0, t1, delta;
+};
+struct WaveParams {
+    int kind;
+    double b, r, b_over_r;        // Morse
+    double sigma, cpi, kappa;     // Morlet (cpi = c * pi^(-1/4)), MexicanHat (sigma)
+};
+hipError_t launch_wavelet_spectra(const WaveRow* rows, int nrows, WaveParams wp, void* buf, hipStream_t s);
+hipError_t launch_wavelet_pack(const WaveRow* rows, int nrows, int64_t maxlen, const void* buf, void* out,
+                               hipStream_t s);
+hipError_t launch_wavelet_time(const WaveRow* rows, int nrows, int64_t maxlen, WaveParams wp, void* out,
+                               hipStream_t s);
+
 constexpr int BL_WORK_DOUBLES = 1024 + 2;   // k_bl_partial blocks + (mean, std)
 hipError_t launch_baseline(int dtype, const void* x, int64_t count, int64_t b0, int64_t b1, int op, void* out,
                            double* work, hipStream_t s);

@@ -5,6 +5,7 @@
 //   accumulate / finalize  epoch reductions power / ITC          (mneutils.py:42-71)
 //   baseline               Baseline correction                   (base.py:18-68)
 //   normal_time / finish   MexicanHat / Haar rows on the device  (base.py:249-256)
+//   wavelet_*              time-domain wavelets, make_wavelet(s)  (base.py:346-376)
 //
 // K1 is HBM-write bound (8 or 16 B per output point, X re-read from L2): each
 // block evaluates W for one scale f and a 256*V-bin tile ONCE into registers,
@@ -275,6 +276,90 @@ hipError_t launch_normal_finish(const NormalRow* rows, int nrows, int64_t lmax, 
         else
             k_normal_finish<double><<<nrows, 256, 0, s>>>(rows, lmax, interp, (const double2*)buf, (cplx<double>*)table);
     }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Time-domain wavelets (make_wavelet, base.py:346-376).
+// Reverse kinds (Morse, Shannon): the spectrum with its default freq = 1 on
+// t_j = j * (1/f) (np.arange(0, sfreq/f*rwl, 1/f): start 0, so the fill is exact j*step),
+// then rocFFT's unnormalised inverse, then `wavelet_pack`: the centre slice
+// [m//2, m//2*3) of hstack(conj(flip(w)), w), scaled by 1/m as scipy's ifft.
+// Time kinds (Morlet, MexicanHat, Haar): the formula on the zero-mean timeline.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_wavelet_spectra(const WaveRow* __restrict__ rows, WaveParams wp,
+                                                         double2* __restrict__ buf) {
+    const WaveRow r = rows[blockIdx.x];
+    for (int64_t j = threadIdx.x; j < r.m; j += blockDim.x) {
+        const double x = (double)j * r.delta;
+        double v;
+        if (wp.kind == NW_MORSE) {        // wavelets.py:65-74 with freq = 1
+            const double step = x > 0.0 ? 1.0 : (x == 0.0 ? x : 0.0);
+            v = 2.0 * (step * pow(x, wp.b) * exp(wp.b_over_r * (1.0 - pow(x, wp.r))));
+        } else {                          // Shannon, wavelets.py:256-262
+            v = x <= 1.0 ? 1.0 : 0.0;
+        }
+        buf[r.off + j] = double2{v, 0.0};
+    }
+}
+
+hipError_t launch_wavelet_spectra(const WaveRow* rows, int nrows, WaveParams wp, void* buf, hipStream_t s) {
+    if (nrows > 0) k_wavelet_spectra<<<nrows, 256, 0, s>>>(rows, wp, (double2*)buf);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_wavelet_pack(const WaveRow* __restrict__ rows, int64_t maxlen,
+                                                      const double2* __restrict__ buf, double2* __restrict__ out) {
+    const WaveRow r = rows[blockIdx.x];
+    const double fct = 1.0 / (double)r.m;
+    double2* row = out + (int64_t)blockIdx.x * maxlen;
+    for (int64_t j = threadIdx.x; j < maxlen; j += blockDim.x) {
+        double2 v{0.0, 0.0};
+        if (j < r.len) {
+            const int64_t pos = j + r.m / 2;
+            if (pos < r.m) {
+                const double2 w = buf[r.off + (r.m - 1 - pos)];
+                v = double2{w.x * fct, -(w.y * fct)};
+            } else {
+                const double2 w = buf[r.off + (pos - r.m)];
+                v = double2{w.x * fct, w.y * fct};
+            }
+        }
+        row[j] = v;
+    }
+}
+
+hipError_t launch_wavelet_pack(const WaveRow* rows, int nrows, int64_t maxlen, const void* buf, void* out,
+                               hipStream_t s) {
+    if (nrows > 0) k_wavelet_pack<<<nrows, 256, 0, s>>>(rows, maxlen, (const double2*)buf, (double2*)out);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_wavelet_time(const WaveRow* __restrict__ rows, int64_t maxlen, WaveParams wp,
+                                                      double2* __restrict__ out) {
+    const WaveRow r = rows[blockIdx.x];
+    double2* row = out + (int64_t)blockIdx.x * maxlen;
+    for (int64_t j = threadIdx.x; j < maxlen; j += blockDim.x) {
+        double2 v{0.0, 0.0};
+        if (j < r.m) {
+            const double t = j == 0 ? r.t0 : (j == 1 ? r.t1 : __dadd_rn(r.t0, __dmul_rn((double)j, r.delta)));
+            if (wp.kind == NW_MORLET) {   // c pi^-1/4 exp(-t^2/2) (exp(i sigma t) - k), wavelets.py:138-141
+                const double a = __dmul_rn(wp.cpi, exp(__ddiv_rn(-__dmul_rn(t, t), 2.0)));
+                const double ph = __dmul_rn(wp.sigma, t);
+                v = double2{__dmul_rn(a, __dsub_rn(cos(ph), wp.kappa)), __dmul_rn(a, sin(ph))};
+            } else if (wp.kind == NW_MEXICAN_HAT) {
+                v = double2{mexican_hat_f(t, wp.sigma), 0.0};
+            } else {
+                v = double2{haar_f(t), 0.0};
+            }
+        }
+        row[j] = v;
+    }
+}
+
+hipError_t launch_wavelet_time(const WaveRow* rows, int nrows, int64_t maxlen, WaveParams wp, void* out,
+                               hipStream_t s) {
+    if (nrows > 0) k_wavelet_time<<<nrows, 256, 0, s>>>(rows, maxlen, wp, (double2*)out);
     return hipGetLastError();
 }
 

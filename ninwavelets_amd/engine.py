@@ -203,3 +203,21 @@ def execute_multi(plans, x: np.ndarray, out_kind: str = 'cwt') -> np.ndarray:
     L.check(L.lib().nw_execute_multi(arr, len(plans), x.ctypes.data_as(ctypes.c_void_p), nsig,
                                      out.ctypes.data_as(ctypes.c_void_p), OUT_KINDS[out_kind]))
     return out
+
+
+def make_wavelets(kind: str, params, freqs, sfreq: float, real_wave_length: float, device: int = 0) -> list:
+    """Time-domain wavelets of a stock kind on the device (nw_make_wavelets,
+    base.py:346-376): a list of complex128 rows of their true (ragged) lengths."""
+    fr = np.ascontiguousarray(list(freqs), dtype=np.float64)
+    p = np.ascontiguousarray(params if params is not None else [], dtype=np.float64)
+    dp = ctypes.POINTER(ctypes.c_double)
+    ip = ctypes.POINTER(ctypes.c_int64)
+    lens = np.zeros(fr.size, dtype=np.int64)
+    mx = ctypes.c_int64()
+    args = (device, KINDS[kind], p.ctypes.data_as(dp), int(p.size), fr.ctypes.data_as(dp), int(fr.size),
+            float(sfreq), float(real_wave_length))
+    L.check(L.lib().nw_make_wavelets(*args, None, ctypes.byref(mx), lens.ctypes.data_as(ip)))
+    out = np.zeros((fr.size, mx.value), dtype=np.complex128)
+    L.check(L.lib().nw_make_wavelets(*args, out.ctypes.data_as(ctypes.c_void_p), ctypes.byref(mx),
+                                     lens.ctypes.data_as(ip)))
+    return [out[i, :lens[i]].copy() for i in range(fr.size)]

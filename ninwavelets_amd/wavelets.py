@@ -70,6 +70,11 @@ class Morlet(WaveletBase):
     def peak_freq(self, freq: float) -> float:
         return self.sigma / (1. - np.exp(-self.sigma * freq))
 
+    def _time_formula_spec(self):
+        if type(self).formula is not Morlet.formula or type(self).peak_freq is not Morlet.peak_freq:
+            return None
+        return 'morlet', [float(self.sigma), 1.0 if self.k == 0 else 0.0, float(self.c), float(self.k)]
+
     def _analytic(self):
         if (type(self).trans_formula is not Morlet.trans_formula
                 or type(self).peak_freq is not Morlet.peak_freq):
@@ -127,6 +132,10 @@ class MexicanHat(WaveletBase):
             return 'mexican_hat', [float(self.sigma), float(self.sfreq), float(self.real_wave_length)]
         return None
 
+    def _time_formula_spec(self):
+        spec = self._device_normal()
+        return None if spec is None else ('mexican_hat', [float(self.sigma)])
+
 
 class Haar(WaveletBase):
     """Haar wavelet, time-domain table path (wavelets.py:265-280)."""
@@ -148,6 +157,9 @@ class Haar(WaveletBase):
         if cls.formula is Haar.formula and cls.peak_freq is WaveletBase.peak_freq:
             return 'haar', [float(self.sfreq), float(self.real_wave_length)]
         return None
+
+    def _time_formula_spec(self):
+        return None if self._device_normal() is None else ('haar', [])
 
 
 class MorseMNE(Morse):

@@ -255,3 +255,42 @@ def baseline(wave: np.ndarray, sfreq: float, start: float, stop: float, op: str)
         'zlog': lambda: np.log10(wave / m) / np.std(part),      # 68-69
     }
     return ops[op]()
+
+
+# ---------------------------------------------------------------------------
+# Time-domain wavelets, make_wavelet(s) (base.py:346-376).  Reverse mode (Morse,
+# Shannon): ifft of the spectrum on arange(0, sfreq/f*rwl, 1/f) with the spectrum's
+# default freq = 1, then conj-flip + stack + centre slice.  Otherwise (Morlet's Both,
+# MexicanHat / Haar's Normal): the time-domain formula on the zero-mean timeline.
+# ---------------------------------------------------------------------------
+def morlet_formula(tc: np.ndarray, sigma: float = 7., gabor: bool = False) -> np.ndarray:
+    """wavelets.py:138-141."""
+    c, k = morlet_constants(sigma, gabor)
+    return c * np.float_power(np.pi, -1 / 4) * np.exp(-np.square(tc) / 2) * (np.exp(sigma * 1j * tc) - k)
+
+
+def make_wavelet(kind: str, freq: float, sfreq: float = 1000., real_wave_length: float = 1.,
+                 **params) -> np.ndarray:
+    if freq == 0:
+        raise ZeroDivisionError
+    if kind in ('morse', 'shannon'):
+        t = np.arange(0, sfreq / freq * real_wave_length, 1 / freq)          # base.py:191-194
+        spec = (morse_spectrum(t, 1., params.get('b', 17.5), params.get('r', 3.)) if kind == 'morse'
+                else shannon_spectrum(t, 1.))
+        w = ifft(spec)
+        half = int(w.shape[0])
+        both = np.hstack((np.conj(np.flip(w)), w))
+        return both[half // 2: half // 2 * 3]
+    sigma = params.get('sigma', 7.)
+    peak = {'morlet': lambda: morlet_peak(sigma, freq), 'mexican_hat': lambda: MEXICAN_HAT_PEAK,
+            'haar': lambda: 1.}[kind]()
+    total = 1. / peak * freq * 2 * np.pi                                      # base.py:211-216
+    one = 1 / sfreq * 2 * np.pi * freq / peak
+    tl = np.arange(-total / 2, total / 2, one)
+    if kind == 'morlet':
+        return morlet_formula(tl, sigma, params.get('gabor', False))
+    return mexican_hat_formula(tl, sigma) if kind == 'mexican_hat' else haar_formula(tl)
+
+
+def make_wavelets(kind: str, freqs, **kw) -> list:
+    return [make_wavelet(kind, f, **kw) for f in freqs]

@@ -19,7 +19,7 @@ import ninwavelets_amd as nw  # noqa: E402
 
 TOL = {'float64': 1e-12, 'float32': 1e-5}
 ENGINES = ['rocfft', 'auto']
-SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline'))]
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets'))]
 CLASSES = {'morse': nw.Morse, 'morlet': nw.Morlet, 'shannon': nw.Shannon,
            'mexican_hat': nw.MexicanHat, 'haar': nw.Haar}
 
@@ -401,3 +401,29 @@ def test_device_normal_table_equals_host_table(kind, interpolate):
         assert np.max(np.abs(a - b)) <= 1e-13 * max(1.0, np.max(np.abs(b)))
     x = synth(1, 2048, 17)[0].astype(np.float64)
     assert rel_err(dev.cwt(x, freqs), host.cwt(x, freqs)) <= 1e-13
+
+
+# ------------------------------------------------------------------ time-domain wavelets (§8f rank 4)
+WAVELET_CASES = {'morse': (nw.Morse, dict(sfreq=1000)), 'morse_b': (nw.Morse, dict(sfreq=500, b=10., r=2.)),
+                 'shannon': (nw.Shannon, dict(sfreq=1000)), 'morlet': (nw.Morlet, dict(sfreq=1000)),
+                 'morlet_gabor': (nw.Morlet, dict(sfreq=1000, gabor=True)),
+                 'mexican_hat': (nw.MexicanHat, dict(sfreq=1000)), 'haar': (nw.Haar, dict(sfreq=1000))}
+
+
+@pytest.mark.parametrize('name', golden_names('wavelets'))
+def test_make_wavelets_against_reference(name):
+    """make_wavelets (base.py:346-376) on the device (nw_make_wavelets: spectrum + rocFFT
+    inverse + conj-flip slice, or the time-domain formula) against the reference's rows:
+    same ragged lengths and dtypes, values within 1e-13 of each row's peak."""
+    g = load_golden(name)
+    cls, kw = WAVELET_CASES[g['meta']['case']]
+    w = cls(**kw)
+    assert w._device_wavelet_spec() is not None
+    rows = w.make_wavelets(list(g['freqs']))
+    ref = np.split(g['rows'], np.cumsum(g['lens'])[:-1])
+    assert [r.shape for r in rows] == [r.shape for r in ref]
+    assert str(rows[0].dtype) == g['meta']['dtype']
+    for got, want in zip(rows, ref):
+        assert np.max(np.abs(got - want)) <= 1e-13 * max(1e-300, np.max(np.abs(want)))
+    single = w.make_wavelet(float(g['freqs'][2]))
+    np.testing.assert_array_equal(single, rows[2])

@@ -7,7 +7,7 @@ import pytest
 from conftest import golden_names, load_golden
 from oracle import nw_oracle as O
 
-SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline'))]
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets'))]
 
 
 def _params(meta):
@@ -72,3 +72,20 @@ def test_oracle_baseline(name):
         got = O.baseline(g['wave'], m['sfreq'], m['start'], m['stop'], op)
         assert got.dtype == g[op].dtype
         np.testing.assert_array_equal(got, g[op])
+
+
+WAVELET_CASES = {'morse': ('morse', {}), 'morse_b': ('morse', dict(b=10., r=2.)), 'shannon': ('shannon', {}),
+                 'morlet': ('morlet', {}), 'morlet_gabor': ('morlet', dict(gabor=True)),
+                 'mexican_hat': ('mexican_hat', {}), 'haar': ('haar', {})}
+
+
+@pytest.mark.parametrize('name', golden_names('wavelets'))
+def test_oracle_make_wavelets(name):
+    """Time-domain wavelets (base.py:346-376) against the reference's own outputs."""
+    g = load_golden(name)
+    kind, params = WAVELET_CASES[g['meta']['case']]
+    rows = O.make_wavelets(kind, g['freqs'], sfreq=g['meta']['sfreq'], **params)
+    ref = np.split(g['rows'], np.cumsum(g['lens'])[:-1])
+    for got, want in zip(rows, ref):
+        assert got.shape == want.shape
+        np.testing.assert_array_equal(got.astype(np.complex128), want)
