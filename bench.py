@@ -104,9 +104,31 @@ def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0):
             if el >= budget_s:
                 break
     return {'value': rows_done * n / el, 'unit': 'points/s', 'cores': 1, 'kind': 'port',
+            'sample_seconds': el, 'rows_done': rows_done,
             'sample': f'{rows_done} (signal, freq) rows of {n} samples over {sigs} signal(s) '
                       f'({kind} {out_kind}, oracle/nw_oracle.py single process, wavelet rows '
                       f'cached), {el:.1f} s'}
+
+
+def _pool_worker(args):
+    kind, n, freqs, out_kind, budget_s, seed = args
+    import numpy as _np
+    r = cpu_baseline(kind, n, _np.asarray(freqs), out_kind, budget_s)
+    return r['value'] * r['sample_seconds'], r['sample_seconds'], r['rows_done']
+
+
+def cpu_baseline_pool(kind, n, freqs, out_kind, budget_s=8.0, workers=16):
+    """The same oracle work in a multiprocessing Pool over signals (BASELINE.md §3 mode b):
+    each worker times its own bounded sample; the rate is the sum of the workers' rates."""
+    import multiprocessing as mp
+    workers = max(1, min(workers, os.cpu_count() or 1))
+    with mp.get_context('spawn').Pool(workers) as pool:
+        res = pool.map(_pool_worker, [(kind, n, list(freqs), out_kind, budget_s, i) for i in range(workers)])
+    rate = sum(pts / el for pts, el, _ in res)
+    rows = sum(r for _, _, r in res)
+    return {'value': rate, 'unit': 'points/s', 'cores': workers, 'kind': 'port',
+            'sample': f'{rows} (signal, freq) rows of {n} samples over {workers} processes '
+                      f'(multiprocessing Pool, each ~{budget_s:.0f} s; sum of per-process rates)'}
 
 
 def main():
@@ -206,10 +228,15 @@ def main():
                 'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
         stage_ms = {k: round(st[k] / args.steps, 3) for k in
                     ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_copy')}
-        cpu = None
+        cpu = cpu_pool = None
         if world == 1 and not args.no_cpu_baseline:
             log('[bench] cpu baseline ...')
             cpu = cpu_baseline(kind, n, freqs, out_kind)
+            for k in ('sample_seconds', 'rows_done'):
+                cpu.pop(k)
+            if n <= (1 << 16):
+                log('[bench] cpu baseline (process pool) ...')
+                cpu_pool = cpu_baseline_pool(kind, n, freqs, out_kind)
         line = {
             'metric': 'CWT throughput (epochs*chans*samples*freqs)/s',
             'value': value, 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
@@ -218,7 +245,7 @@ def main():
             'config': {'workload': text, 'wavelet': kind, 'epochs': epochs * world, 'chans': chans,
                        'samples': n, 'freqs': F, 'output': out_kind, 'engine': st['engine'],
                        'chunk_signals': C, 'parallelism': f'dp{world} (signals sharded, no collective)'},
-            'roofline': roof, 'cpu_baseline': cpu, 'stage_ms_per_step': stage_ms,
+            'roofline': roof, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool, 'stage_ms_per_step': stage_ms,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
