@@ -142,6 +142,7 @@ def main():
     ap.add_argument('--epochs', type=int, default=None, help='override epochs per GPU')
     ap.add_argument('--output', default=None, choices=['cwt', 'abs', 'power'],
                     help='override the config\'s output kind (diagnostics)')
+    ap.add_argument('--samples', type=int, default=None, help='override the signal length (diagnostics)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 
@@ -164,6 +165,8 @@ def main():
         epochs = args.epochs
     if args.output:
         out_kind = args.output
+    if args.samples:
+        n = args.samples
     S = epochs * chans                       # signals on this rank
     F = len(freqs)
     C = min(args.chunk, S)

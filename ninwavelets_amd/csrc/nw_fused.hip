@@ -346,7 +346,11 @@ template <int N, int E, int P> struct PassInfo {
     static constexpr int Q = E / R;
     static constexpr int STRIDE = N / R;
     static constexpr bool LAST = (P == G::npass() - 1);
-    static constexpr bool PAIRED = LAST && Q >= 2;
+    // pairs (j = Q*t + q) only when Q == 2: the two outputs of a lane are then adjacent AND
+    // neighbouring lanes are too (16-B stores, whole lines).  At Q >= 4 pairing put lanes Q
+    // outputs apart (a store instruction touched 1/2 .. 1/4 of each line: 4x slower at
+    // n = 8192); the lane-contiguous j = t + q*T plus DPP packing keeps stores whole.
+    static constexpr bool PAIRED = LAST && Q == 2;
     static_assert(STRIDE % E == 0 && NS % E == 0, "pad must stay linear");
     __device__ static __forceinline__ int bfly(int t, int q) { return PAIRED ? Q * t + q : t + q * G::T; }
 };
@@ -489,9 +493,10 @@ struct LastStores {
     static constexpr int R = I::R, Q = I::Q;
     static constexpr int STEP = I::PAIRED ? 2 : 1;
     static constexpr int PACK_W = (int)(16 / sizeof(O));
-    static constexpr int PACK = (!I::PAIRED && Q == 1 && NW_PACK_STORES && PACK_W <= NW_PACK_MAX) ? PACK_W : 1;
+    static constexpr int PACK = (!I::PAIRED && NW_PACK_STORES && PACK_W <= NW_PACK_MAX && R % PACK_W == 0)
+                                    ? PACK_W : 1;
     static_assert(PACK == 1 || PACK == 2 || PACK == 4, "pack");
-    static constexpr int COUNT = PACK > 1 ? R / PACK : Q / STEP * R;   // store instructions per thread per signal
+    static constexpr int COUNT = PACK > 1 ? Q * R / PACK : Q / STEP * R;   // store instructions per thread per signal
     // all stores of one signal (v: the last pass's registers, bit-reversed rows)
     __device__ static __forceinline__ void all(const C2<T>* v, void* orow, int t) {
         if constexpr (PACK == 1) {
@@ -500,10 +505,11 @@ struct LastStores {
             const int c = t & (PACK - 1);
             const uint32_t lane = (uint32_t)((t & ~(PACK - 1)) + I::NS * c) * (uint32_t)sizeof(O);
 #pragma unroll
-            for (int g = 0; g < R / PACK; ++g) {
+            for (int qg = 0; qg < Q * (R / PACK); ++qg) {
+                const int q = qg / (R / PACK), g = qg % (R / PACK);   // butterfly t + q*T, row group g
                 O val[PACK];
 #pragma unroll
-                for (int b = 0; b < PACK; ++b) val[b] = out_value<OUT, T>(v[bitrev<R>(g * PACK + b)]);
+                for (int b = 0; b < PACK; ++b) val[b] = out_value<OUT, T>(v[q * R + bitrev<R>(g * PACK + b)]);
                 if constexpr (PACK >= 2) {
                     const bool hi1 = c & 1;
 #pragma unroll
@@ -522,9 +528,10 @@ struct LastStores {
 #ifdef NW_ABL_NOSTORE
                 asm volatile("" ::"v"(__builtin_bit_cast(V, pk)));
 #else
-                __builtin_nontemporal_store(__builtin_bit_cast(V, pk),
-                                            reinterpret_cast<V*>(at(reinterpret_cast<P16*>(orow), lane,
-                                                                    (uint32_t)(g * PACK * I::NS * sizeof(O)))));
+                __builtin_nontemporal_store(
+                    __builtin_bit_cast(V, pk),
+                    reinterpret_cast<V*>(at(reinterpret_cast<P16*>(orow), lane,
+                                            (uint32_t)((q * Geometry<N, E>::T + g * PACK * I::NS) * sizeof(O)))));
 #endif
             }
         }
@@ -1005,8 +1012,14 @@ bool fused_supported(int64_t n, int dtype) {
     return dtype == NW_F32 ? n <= 16384 : (dtype == NW_F64 && n <= 8192);
 }
 
+#ifndef NW_E4096
+#define NW_E4096 16   // E = 32 measured slower here (0.350 -> 0.404 ms power)
+#endif
+#ifndef NW_E8192
+#define NW_E8192 32   // measured: n = 8192 power 0.887 -> 0.768 ms, cwt 1.034 -> 0.926 ms vs E = 16
+#endif
 #define NW_FUSED_TABLE(X)                                                               \
-    X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, 16) X(float, 8192, 16)        \
+    X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, NW_E4096) X(float, 8192, NW_E8192) \
     X(float, 16384, NW_E16384) X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) \
     X(double, 8192, 16)
 
