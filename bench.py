@@ -46,11 +46,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def synth_device(torch, S, n, seed, device, sfreq=1000.):
+def synth_device(torch, S, n, seed, device, sfreq=1000., dtype=None):
     """Synthetic multi-channel sinusoids + noise, generated on the device."""
+    dtype = dtype or torch.float32
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    x = torch.empty((S, n), dtype=torch.float32, device=device)
+    x = torch.empty((S, n), dtype=dtype, device=device)
     t = torch.arange(n, device=device, dtype=torch.float64) / sfreq
     step = 1024
     for s0 in range(0, S, step):
@@ -58,7 +59,7 @@ def synth_device(torch, S, n, seed, device, sfreq=1000.):
         fc = torch.rand((s1 - s0, 1), generator=g, device=device, dtype=torch.float64) * 99 + 1
         ph = torch.rand((s1 - s0, 1), generator=g, device=device, dtype=torch.float64) * 2 * np.pi
         noise = torch.randn((s1 - s0, n), generator=g, device=device, dtype=torch.float32)
-        x[s0:s1] = (torch.sin(2 * np.pi * fc * t + ph)).float() + 0.1 * noise
+        x[s0:s1] = ((torch.sin(2 * np.pi * fc * t + ph)) + 0.1 * noise).to(dtype)
     return x
 
 
@@ -143,6 +144,8 @@ def main():
     ap.add_argument('--output', default=None, choices=['cwt', 'abs', 'power'],
                     help='override the config\'s output kind (diagnostics)')
     ap.add_argument('--samples', type=int, default=None, help='override the signal length (diagnostics)')
+    ap.add_argument('--dtype', default=None, choices=['float32', 'float64'],
+                    help='override the compute dtype (diagnostics)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 
@@ -167,18 +170,22 @@ def main():
         out_kind = args.output
     if args.samples:
         n = args.samples
+    if args.dtype:
+        dtype = args.dtype
     S = epochs * chans                       # signals on this rank
     F = len(freqs)
     C = min(args.chunk, S)
-    x = synth_device(torch, S, n, seed=1000 + rank, device=dev)
-    odt = torch.complex64 if out_kind == 'cwt' else torch.float32
+    f64 = dtype == 'float64'
+    x = synth_device(torch, S, n, seed=1000 + rank, device=dev, dtype=torch.float64 if f64 else torch.float32)
+    odt = {('cwt', False): torch.complex64, ('cwt', True): torch.complex128}.get(
+        (out_kind, f64), torch.float64 if f64 else torch.float32)
     bufs = [torch.empty((C, F, n), dtype=odt, device=dev) for _ in range(1 if C >= S else 2)]
     plan = nw.Plan(n, F, dtype, device=local, max_batch=C,
                    engine=None if args.engine == 'auto' else args.engine, timing=True)
     grid = L.trans_grid(n / 1000., 1000., False)
     params = {'morse': [17.5, 3.0], 'morlet': [7.0, 0.0]}[kind]
     plan.set_wavelet(kind, params, freqs, grid)
-    esz = 4
+    esz = 8 if f64 else 4
     x_ptr, x_row = x.data_ptr(), n * esz
 
     def step():
@@ -244,7 +251,7 @@ def main():
             'metric': 'CWT throughput (epochs*chans*samples*freqs)/s',
             'value': value, 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f32', 'data': 'synthetic',
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64' if f64 else 'f32', 'data': 'synthetic',
             'config': {'workload': text, 'wavelet': kind, 'epochs': epochs * world, 'chans': chans,
                        'samples': n, 'freqs': F, 'output': out_kind, 'engine': st['engine'],
                        'chunk_signals': C, 'parallelism': f'dp{world} (signals sharded, no collective)'},
