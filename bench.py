@@ -223,21 +223,46 @@ def main():
     if rank == 0:
         # dominant kernel: the fused kernel, or K1 (the spectrum multiply) on the rocFFT engine
         fused = st['engine'] == 'fused'
+        two_pass = fused and st['launches_rows'] > 0     # n > 16384: nw_large.hip
         launches = st['launches_fused'] if fused else st['launches_multiply']
         ms = (st['ms_fused'] if fused else st['ms_multiply']) / max(1, launches)
         out_e = (2 if out_kind == 'cwt' else 1) * esz
         if not fused:
             out_e = 2 * esz                    # K1 always writes the complex product
-        per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
+        extra = {}
+        if two_pass:
+            # column pass (the kernel that writes the output): reads B once (8 B/pt, complex
+            # fp32) and writes each output point once; the row pass writes B once and reads
+            # the transposed spectrum Xt once per launch (from L2 across the scales of a tile)
+            pts_launch = float(S) * F * n * args.steps / max(1, launches)
+            per_launch = pts_launch * (8 + out_e)
+            rows_l = max(1, st['launches_rows'])
+            rows_pts = float(S) * F * n * args.steps / rows_l
+            rows_bytes = rows_pts * 8 + n * 8
+            rows_ms = st['ms_rows'] / rows_l
+            kname = 'cols_kernel'
+            extra['roofline_rows'] = {
+                'kernel': 'rows_kernel', 'bound': 'hbm',
+                'achieved': round(rows_bytes / (rows_ms * 1e-3) / 1e9, 1), 'peak': PEAK_HBM_GBPS,
+                'unit': 'GB/s', 'frac': round(rows_bytes / (rows_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+                'avg_launch_ms': round(rows_ms, 4), 'algorithmic_bytes_per_launch': rows_bytes}
+            # end to end against the path's minimum traffic (X read once, every output once)
+            min_bytes = float(S) * ((n // 2 + 1) * 2 * esz + F * n * out_e)
+            extra['end_to_end_min_traffic'] = {
+                'bytes_per_step': min_bytes,
+                'achieved': round(min_bytes / (el / args.steps) / 1e9, 1), 'unit': 'GB/s',
+                'frac': round(min_bytes / (el / args.steps) / 1e9 / PEAK_HBM_GBPS, 4)}
+        else:
+            per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
+            kname = 'nw_fused' if fused else 'k1_multiply'
         achieved = per_launch / (ms * 1e-3) / 1e9
-        kname = 'nw_fused' if fused else 'k1_multiply'
         roof = {'kernel': kname, 'bound': 'hbm',
                 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
                 'frac': round(achieved / PEAK_HBM_GBPS, 4),
                 'traffic': pmc_traffic(kname, args.config, C, st['engine']),
                 'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
         stage_ms = {k: round(st[k] / args.steps, 3) for k in
-                    ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_copy')}
+                    ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_rows', 'ms_copy')}
         cpu = cpu_pool = None
         if world == 1 and not args.no_cpu_baseline:
             log('[bench] cpu baseline ...')
@@ -255,7 +280,7 @@ def main():
             'config': {'workload': text, 'wavelet': kind, 'epochs': epochs * world, 'chans': chans,
                        'samples': n, 'freqs': F, 'output': out_kind, 'engine': st['engine'],
                        'chunk_signals': C, 'parallelism': f'dp{world} (signals sharded, no collective)'},
-            'roofline': roof, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool, 'stage_ms_per_step': stage_ms,
+            'roofline': roof, **extra, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool, 'stage_ms_per_step': stage_ms,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -96,10 +96,14 @@ typedef struct nw_stats {
     double  ms_inverse;     /* rocFFT inverse (rocFFT engine) */
     double  ms_epilogue;    /* K2 |.| / |.|^2 (rocFFT engine) */
     double  ms_fused;       /* fused multiply + inverse FFT + epilogue (fused engine) */
-    double  ms_copy;        /* host<->device copies */
+    double  ms_copy;        /* copies (host<->device, input staging, spectrum transposes) */
     int64_t launches_multiply;
     int64_t launches_fused;
     int64_t engine;         /* NW_ENGINE_ROCFFT or NW_ENGINE_FUSED actually used */
+    double  ms_rows;        /* fused engine, n > 16384: pass-1 row FFTs (ms_fused then times
+                               pass 2, the column FFTs + epilogue; the spectrum transpose is
+                               timed in ms_copy) */
+    int64_t launches_rows;
 } nw_stats;
 
 typedef struct nw_plan nw_plan;

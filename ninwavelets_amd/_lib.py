@@ -48,7 +48,8 @@ class nw_stats(ctypes.Structure):
                 ('ms_inverse', ctypes.c_double), ('ms_epilogue', ctypes.c_double),
                 ('ms_fused', ctypes.c_double), ('ms_copy', ctypes.c_double),
                 ('launches_multiply', ctypes.c_int64), ('launches_fused', ctypes.c_int64),
-                ('engine', ctypes.c_int64)]
+                ('engine', ctypes.c_int64), ('ms_rows', ctypes.c_double),
+                ('launches_rows', ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -65,7 +65,7 @@ struct DeviceGuard {
     }
 };
 
-enum Stage { ST_FWD = 0, ST_MUL, ST_INV, ST_EPI, ST_FUSED, ST_COPY, ST_N };
+enum Stage { ST_FWD = 0, ST_MUL, ST_INV, ST_EPI, ST_FUSED, ST_COPY, ST_ROWS, ST_N };
 
 struct Pending {
     int stage;
@@ -103,9 +103,12 @@ struct nw_plan {
     size_t d_out_bytes = 0;
     void* d_acc = nullptr;           // epoch reductions: fp64 (F, n) sums (x2 for phases)
     size_t d_acc_bytes = 0;
-    void* d_wtab = nullptr;          // fused engine: W[f, k] (pad_to + 1/n applied)
+    void* d_wtab = nullptr;          // fused engine: W[f, k] (pad_to + 1/n applied); n > 16384: kmax[f]
     size_t d_wtab_bytes = 0;
     bool wtab_valid = false;
+    bool large = false;              // fused engine, two-pass form (nw_large.hip)
+    void* d_scratch = nullptr;       // two-pass form: Xt + B
+    size_t d_scratch_bytes = 0;
 
     // rocFFT, keyed by batch count
     std::map<int64_t, rocfft_plan> fwd, inv;
@@ -149,8 +152,19 @@ int take_event(nw_plan* p, hipEvent_t* ev) {
 }
 
 // Run `fn` on the plan stream, bracketed by events when NW_TIMING is set.
+// launch counts are kept with or without NW_TIMING (they tell which kernels ran)
+void count_launch(nw_plan* p, int stage) {
+    switch (stage) {
+        case ST_MUL: p->stats.launches_multiply++; break;
+        case ST_FUSED: p->stats.launches_fused++; break;
+        case ST_ROWS: p->stats.launches_rows++; break;
+        default: break;
+    }
+}
+
 template <typename F>
 int staged(nw_plan* p, int stage, F&& fn) {
+    count_launch(p, stage);
     if (!(p->flags & NW_TIMING)) return fn();
     Pending pe{stage, nullptr, nullptr};
     NW_TRY(take_event(p, &pe.a));
@@ -170,10 +184,11 @@ int resolve_timing(nw_plan* p) {
         NW_HIP(hipEventElapsedTime(&ms, pe.a, pe.b));
         switch (pe.stage) {
             case ST_FWD: p->stats.ms_forward += ms; break;
-            case ST_MUL: p->stats.ms_multiply += ms; p->stats.launches_multiply++; break;
+            case ST_MUL: p->stats.ms_multiply += ms; break;
             case ST_INV: p->stats.ms_inverse += ms; break;
             case ST_EPI: p->stats.ms_epilogue += ms; break;
-            case ST_FUSED: p->stats.ms_fused += ms; p->stats.launches_fused++; break;
+            case ST_FUSED: p->stats.ms_fused += ms; break;
+            case ST_ROWS: p->stats.ms_rows += ms; break;
             default: p->stats.ms_copy += ms; break;
         }
         p->event_pool.push_back(pe.a);
@@ -255,6 +270,39 @@ int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind
                             (size_t)p->nh * 2 * p->esz);
     }));
 
+    if (!rocfft_engine && p->large) {
+        // two-pass form (n > 16384): per signal, X -> Xt, then per chunk of scales the
+        // row pass (W * X, length-N2 FFTs) into B and the column pass (length-N1 FFTs +
+        // epilogue) into the destination rows
+        if (!p->wtab_valid) {
+            NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes, nw::large_support_bytes(p->nfreq)));
+            NW_HIP(nw::build_large_support(p->desc, p->d_wtab, p->stream));
+            p->wtab_valid = true;
+        }
+        NW_TRY(ensure(&p->d_scratch, &p->d_scratch_bytes, nw::large_scratch_bytes(p->n, p->nfreq)));
+        const size_t out_row = (size_t)p->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
+        const int64_t fc = nw::large_fchunk(p->n, p->nfreq);
+        for (int64_t sidx = 0; sidx < c; ++sidx) {
+            const char* Xs = (const char*)p->d_X + (size_t)sidx * p->nh * 2 * p->esz;
+            char* os = (char*)dst + (size_t)sidx * p->nfreq * out_row;
+            NW_TRY(staged(p, ST_COPY, [&] {   // the spectrum transpose: timed with the copies
+                NW_HIP(nw::large_transpose(p->desc, Xs, p->d_scratch, p->stream));
+                return NW_OK;
+            }));
+            for (int64_t f0 = 0; f0 < p->nfreq; f0 += fc) {
+                const int nf = (int)std::min<int64_t>(fc, p->nfreq - f0);
+                NW_TRY(staged(p, ST_ROWS, [&] {
+                    NW_HIP(nw::large_rows(p->desc, (int)f0, nf, p->d_wtab, p->d_scratch, p->stream));
+                    return NW_OK;
+                }));
+                NW_TRY(staged(p, ST_FUSED, [&] {
+                    NW_HIP(nw::large_cols(p->desc, out_kind, (int)f0, nf, p->d_scratch, os, p->stream));
+                    return NW_OK;
+                }));
+            }
+        }
+        return NW_OK;
+    }
     if (!rocfft_engine) {
         if (!p->wtab_valid) {
             NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes,
@@ -413,7 +461,7 @@ void free_plan(nw_plan* p) {
     for (auto& kv : p->inv) rocfft_plan_destroy(kv.second);
     if (p->info) rocfft_execution_info_destroy(p->info);
     void* bufs[] = {p->work,   p->d_x,    p->d_X,        p->d_Y,     p->d_out,      p->d_wtab,
-                    p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len, p->d_acc};
+                    p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len, p->d_acc, p->d_scratch};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& pe : p->pending) {
@@ -481,7 +529,9 @@ int nw_trans_grid(double real_length, double sfreq, int interpolate, nw_grid* g)
     return NW_OK;
 }
 
-int nw_fused_supported(int64_t n, int dtype) { return nw::fused_supported(n, dtype) ? 1 : 0; }
+int nw_fused_supported(int64_t n, int dtype) {
+    return nw::fused_supported(n, dtype) || nw::large_supported(n, dtype) ? 1 : 0;
+}
 
 int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int32_t nfreq, int dtype,
                    uint32_t flags) {
@@ -507,7 +557,8 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     p->dtype = dtype;
     p->flags = flags;
     p->esz = dtype == NW_F32 ? 4 : 8;
-    const bool fused_ok = nw::fused_supported(n, dtype);
+    const bool large_ok = !nw::fused_supported(n, dtype) && nw::large_supported(n, dtype);
+    const bool fused_ok = nw::fused_supported(n, dtype) || large_ok;
     if (flags & NW_ENGINE_FUSED) {
         if (!fused_ok) {
             free_plan(p);
@@ -519,6 +570,7 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     } else {
         p->engine = fused_ok ? NW_ENGINE_FUSED : NW_ENGINE_ROCFFT;
     }
+    p->large = p->engine == NW_ENGINE_FUSED && large_ok;
     p->stats.engine = p->engine;
     auto bail = [&](int code) {
         free_plan(p);
@@ -535,7 +587,7 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     sz = 0;
     r = ensure(&p->d_X, &sz, (size_t)max_batch * p->nh * 2 * p->esz);
     if (r != NW_OK) return bail(r);
-    if (p->engine == NW_ENGINE_FUSED) {
+    if (p->engine == NW_ENGINE_FUSED && !p->large) {
         e = nw::fused_prepare(n, dtype);
         if (e != hipSuccess) return bail(fail(NW_E_HIP, std::string("fused_prepare: ") + hipGetErrorString(e)));
     }

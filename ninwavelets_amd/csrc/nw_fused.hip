@@ -20,644 +20,11 @@
 #include <mutex>
 #include <tuple>
 
-#include "nw_internal.h"
-
-#ifndef NW_HWTWIDDLE
-#define NW_HWTWIDDLE 1   // fp32 twiddles from v_cos/v_sin (no loads); fp64 always uses the table
-#endif
-#ifndef NW_PACK_STORES
-#define NW_PACK_STORES 1   // unpaired last pass: lane-pair transposes -> 16-B stores
-#endif
-#ifndef NW_PACK_MAX
-#define NW_PACK_MAX 2      // measured (n = 4096): pairs of 8-B outputs 0.413 -> 0.403 ms (cwt);
-                           // quads of 4-B outputs 0.337 -> 0.360 ms (power): slower, so off
-#endif
-#ifndef NW_PRUNE
-#define NW_PRUNE 1         // pass 0 skips the elements beyond the W row's support
-#endif
-#ifndef NW_PRUNE_MIN
-#define NW_PRUNE_MIN 4     // smallest pass-0 variant (support rounded up to it; 1 and 2 add
-                           // code without a measurable gain)
-#endif
-#ifndef NW_XDMA_MIN_E
-#define NW_XDMA_MIN_E 32 // fp32 with E >= this: the next signal's X copied into the idle LDS
-                         // image by LDS-DMA before the stores (measured: E=32 1.99 -> 1.94 ms,
-                         // E=16 0.362 -> 0.386 ms, so off there)
-#endif
+#include "nw_fft_dev.h"
 
 namespace nw {
 
 namespace {
-
-template <typename T> struct C2 {
-    T re, im;
-};
-
-template <typename T> __device__ __forceinline__ C2<T> cmul(C2<T> a, C2<T> b) {
-    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
-}
-
-// --- memory ops addressed as wave-uniform base (SGPR pair) + 32-bit per-lane byte
-// offset: `global_load/store ... v_off, s[base:base+1]` (saddr form), i.e. one VGPR
-// per address instead of a 64-bit pair.  The empty asm makes the offset opaque so
-// the compiler cannot re-associate constant parts back into 64-bit address math.
-// (The raw_buffer_load/store_b64 builtins of this toolchain emit a single dword
-// and are not used.)
-//
-// `lane_off` is a per-thread byte offset shared by many accesses and `c` a
-// compile-time byte offset.  The volatile asm re-materialises lane_off at every
-// use, so neither it nor lane_off + c can be hoisted out of the signal loop as a
-// per-element loop invariant (which left ~100 live offsets and spilled).
-template <typename P>
-__device__ __forceinline__ P* at(P* base, uint32_t lane_off, uint32_t c = 0) {
-    asm volatile("" : "+v"(lane_off));
-    return reinterpret_cast<P*>(reinterpret_cast<char*>(base) + (lane_off + c));
-}
-template <typename P>
-__device__ __forceinline__ const P* at(const P* base, uint32_t lane_off, uint32_t c = 0) {
-    asm volatile("" : "+v"(lane_off));
-    return reinterpret_cast<const P*>(reinterpret_cast<const char*>(base) + (lane_off + c));
-}
-
-// cos(2*pi*i/32), i = 0..31
-__device__ constexpr double kCos32[32] = {
-    1.0, 0.98078528040323043, 0.92387953251128674, 0.83146961230254524, 0.70710678118654757,
-    0.55557023301960218, 0.38268343236508978, 0.19509032201612825, 0.0, -0.19509032201612825,
-    -0.38268343236508978, -0.55557023301960218, -0.70710678118654757, -0.83146961230254524,
-    -0.92387953251128674, -0.98078528040323043, -1.0, -0.98078528040323043, -0.92387953251128674,
-    -0.83146961230254524, -0.70710678118654757, -0.55557023301960218, -0.38268343236508978,
-    -0.19509032201612825, 0.0, 0.19509032201612825, 0.38268343236508978, 0.55557023301960218,
-    0.70710678118654757, 0.83146961230254524, 0.92387953251128674, 0.98078528040323043};
-
-// a * exp(+2 pi i K / LEN) for compile-time K, LEN (LEN | 32); trivial angles special-cased
-template <typename T, int K, int LEN>
-__device__ __forceinline__ C2<T> twc(C2<T> a) {
-    constexpr int idx = K * (32 / LEN);
-    if constexpr (idx == 0) {
-        return a;
-    } else if constexpr (idx == 8) {                  // +i
-        return {-a.im, a.re};
-    } else if constexpr (idx == 4) {                  // (1+i)/sqrt2
-        constexpr T h = (T)0.70710678118654757;
-        return {h * (a.re - a.im), h * (a.re + a.im)};
-    } else if constexpr (idx == 12) {                 // (-1+i)/sqrt2
-        constexpr T h = (T)0.70710678118654757;
-        return {-h * (a.re + a.im), h * (a.re - a.im)};
-    } else {
-        constexpr T c = (T)kCos32[idx];
-        constexpr T s = (T)kCos32[(idx + 24) % 32];   // sin(x) = cos(x - pi/2)
-        return {a.re * c - a.im * s, a.re * s + a.im * c};
-    }
-}
-
-template <int R> __host__ __device__ constexpr int bitrev(int i) {
-    int r = 0;
-    for (int b = 1; b < R; b <<= 1) {
-        r = (r << 1) | (i & 1);
-        i >>= 1;
-    }
-    return r;
-}
-
-// radix-2 DIF butterflies of one stage (half size H), unrolled by template recursion.
-// NZ: only the first NZ elements of every group of 2H are nonzero (pruned inputs): a
-// butterfly whose partner is zero is a copy plus a twiddle, one with both zero is skipped
-// (exact: u + 0 = u), and every group keeps a nonzero prefix of min(NZ, H) after the stage.
-template <typename T, int R, int H, int G, int K, int NZ>
-__device__ __forceinline__ void dif_bfly(C2<T>* a) {
-    if constexpr (G < R) {
-        if constexpr (K < H) {
-            if constexpr (K + H < NZ) {
-                const C2<T> u = a[G + K], w = a[G + K + H];
-                a[G + K] = {u.re + w.re, u.im + w.im};
-                a[G + K + H] = twc<T, K, 2 * H>(C2<T>{u.re - w.re, u.im - w.im});
-            } else if constexpr (K < NZ) {
-                a[G + K + H] = twc<T, K, 2 * H>(a[G + K]);
-            }
-            dif_bfly<T, R, H, G, K + 1, NZ>(a);
-        } else {
-            dif_bfly<T, R, H, G + 2 * H, 0, NZ>(a);
-        }
-    }
-}
-
-template <typename T, int R, int H, int NZ>
-__device__ __forceinline__ void dif_stages(C2<T>* a) {
-    if constexpr (H >= 1) {
-        dif_bfly<T, R, H, 0, 0, NZ>(a);
-        dif_stages<T, R, H / 2, (NZ < H ? NZ : H)>(a);
-    }
-}
-
-// inverse DFT of R registers, natural-order input, bit-reversed output; inputs r >= NZ
-// are zero (their registers must hold zeros)
-template <typename T, int R, int NZ = R>
-__device__ __forceinline__ void idft_br(C2<T>* v) {
-    if constexpr (R > 1) dif_stages<T, R, R / 2, NZ>(v);
-}
-
-template <int R> constexpr int ilog2() { return R <= 1 ? 0 : 1 + ilog2<R / 2>(); }
-
-// v[r] *= w^(r m), w = exp(2 pi i / NSR), r = 1..R-1.  The base powers w^(m 2^k)
-// come from the exact table tw[i] = exp(2 pi i i / N) (L2-resident); every other
-// power is a product of at most log2(R) of them: a few ulp, no recurrence drift.
-// The bases are loaded a phase ahead of use (before the LDS exchange that feeds
-// the pass) so the table latency hides under the exchange.
-template <typename T, int R, int N, int NSR>
-__device__ __forceinline__ void twiddle_bases(C2<T>* p, int m, const C2<T>* __restrict__ tw) {
-    // the twiddles depend on the thread only: keep the compiler from hoisting all of
-    // them out of the signal loop (that keeps ~120 values live and spills)
-    asm volatile("" : "+v"(m));
-#pragma unroll
-    for (int k = 0; k < ilog2<R>(); ++k) {
-        if constexpr (sizeof(T) == 4 && NW_HWTWIDDLE) {
-            // v_cos/v_sin take revolutions; (m << k) / NSR is exact in fp32 (power-of-two
-            // denominator), measured max abs error 1.2e-7 over all 16384 angles: no memory
-            // access, so nothing queues behind this wave's in-flight stores
-            const float rev = (float)(m << k) * (1.0f / (float)NSR);
-            p[k] = C2<T>{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
-        } else {
-            p[k] = *at(tw, (uint32_t)m * (uint32_t)((N / NSR) * sizeof(C2<T>)) << k);
-        }
-    }
-}
-template <typename T, int R>
-__device__ __forceinline__ void twiddle_apply(C2<T>* v, const C2<T>* p) {
-    constexpr int LR = ilog2<R>();
-#pragma unroll
-    for (int r = 1; r < R; ++r) {
-        C2<T> w = p[__builtin_ctz(r)];
-#pragma unroll
-        for (int k = __builtin_ctz(r) + 1; k < LR; ++k)
-            if (r & (1 << k)) w = cmul(w, p[k]);
-        v[r] = cmul(v[r], w);
-    }
-}
-
-// Padded LDS half image (one real component at a time): 2 extra slots after every
-// kPadG<E> slots (E = elements per thread; 32 slots for E = 16, E otherwise).  Pairs
-// stay 8-B aligned, and every access is base(thread) + compile-time offset: bases
-// mod kPadG plus offsets mod kPadG never carry at the instantiated sizes (checked
-// exhaustively for N = 1024 .. 16384).  Padding every 16 slots at E = 16 made every
-// exchange access 2-way bank-conflicted (a contiguous 32-lane ds_read_b32 wrapped its
-// last two lanes onto banks 0-1; rocprofv3 SQ_LDS_BANK_CONFLICT = 2.2 cycles per LDS
-// instruction at C3); every 32 slots removes them at N = 4096 and leaves 1 in 8
-// elsewhere (bank model: MI355X_MICROARCH.md §LDS).
-template <int E> constexpr int kPadG = E < 32 ? 32 : E;
-template <int E> __device__ __forceinline__ int lds_idx(int i) { return i + 2 * (i / kPadG<E>); }
-template <int E> constexpr int lds_off(int c) { return c + 2 * (c / kPadG<E>); }   // c a multiple of E
-template <int N, int E> constexpr int lds_elems() { return N + 2 * (N / kPadG<E>); }
-
-template <int N, int E> struct Geometry {
-    static constexpr int T = N / E;                 // threads per block
-    static constexpr int radix(int p) {             // radix of pass p; pass 0 has radix E
-        int done = E;
-        for (int i = 1; i < p; ++i) done *= (N / done >= E ? E : N / done);
-        const int left = N / done;
-        return p == 0 ? E : (left >= E ? E : left);
-    }
-    static constexpr int npass() {
-        int done = E, p = 1;
-        while (done < N) {
-            done *= (N / done >= E ? E : N / done);
-            ++p;
-        }
-        return p;
-    }
-    static constexpr int ns(int p) {                // Ns before pass p
-        int done = 1;
-        for (int i = 0; i < p; ++i) done *= radix(i);
-        return done;
-    }
-};
-
-// output value of one point: y, |y| or |y|^2
-template <int OUT, typename T> struct OutT { using type = T; };
-template <typename T> struct OutT<NW_OUT_CWT, T> { using type = C2<T>; };
-template <int OUT, typename T>
-__device__ __forceinline__ typename OutT<OUT, T>::type out_value(C2<T> y) {
-    if constexpr (OUT == NW_OUT_CWT) return y;
-    else if constexpr (OUT == NW_OUT_POWER) return y.re * y.re + y.im * y.im;
-    else return (T)sqrt(y.re * y.re + y.im * y.im);
-}
-
-// store outputs idx, idx+1 of the current row (orow: wave-uniform row base) as ONE
-// vector store (16 B for complex64, 8 B for float32, 2x16 B for complex128)
-// outputs lane_idx + c_idx (pair: and the next one) of the current row
-template <int OUT, typename T>
-__device__ __forceinline__ void store_pair(void* orow, uint32_t lane_idx, uint32_t c_idx, C2<T> y0, C2<T> y1) {
-    using O = typename OutT<OUT, T>::type;
-    struct alignas(2 * sizeof(O)) P2 { O a, b; };
-#ifdef NW_ABL_NOSTORE
-    asm volatile("" ::"v"(y0.re), "v"(y0.im), "v"(y1.re), "v"(y1.im), "v"(lane_idx));
-    return;
-#endif
-#ifndef NW_PLAIN_STORE   // streaming (nt) stores: measured 5 % faster than plain at n = 16384
-    using V = typename std::conditional<sizeof(P2) == 16, float __attribute__((ext_vector_type(4))),
-              typename std::conditional<sizeof(P2) == 8, float __attribute__((ext_vector_type(2))),
-                                        double __attribute__((ext_vector_type(4)))>::type>::type;
-    const P2 pv{out_value<OUT, T>(y0), out_value<OUT, T>(y1)};
-    __builtin_nontemporal_store(__builtin_bit_cast(V, pv),
-                                reinterpret_cast<V*>(at(reinterpret_cast<P2*>(orow), lane_idx * (uint32_t)sizeof(O),
-                                                        c_idx * (uint32_t)sizeof(O))));
-#else
-    *at(reinterpret_cast<P2*>(orow), lane_idx * (uint32_t)sizeof(O), c_idx * (uint32_t)sizeof(O)) =
-        P2{out_value<OUT, T>(y0), out_value<OUT, T>(y1)};
-#endif
-}
-template <int OUT, typename T>
-__device__ __forceinline__ void store_one(void* orow, uint32_t lane_idx, uint32_t c_idx, C2<T> y) {
-    using O = typename OutT<OUT, T>::type;
-#ifdef NW_ABL_NOSTORE
-    asm volatile("" ::"v"(y.re), "v"(y.im), "v"(lane_idx));
-    return;
-#endif
-    *at(reinterpret_cast<O*>(orow), lane_idx * (uint32_t)sizeof(O), c_idx * (uint32_t)sizeof(O)) =
-        out_value<OUT, T>(y);
-}
-
-// ---- diagnostic phase stamps (NW_STAMPS builds only; never in the product build).
-// Per wave: cycles between consecutive stamps are summed into SGPR-resident
-// counters and lane 0 adds them to g_nw_stamps at the end (cdna_hip_programming.md
-// §7 "In-kernel stamps"): read the SHARES, not the run time of a stamped build.
-#ifdef NW_STAMPS
-constexpr int kStamps = 8;
-__device__ unsigned long long g_nw_stamps[kStamps + 1];
-struct Stamps {
-    unsigned long long last, acc[kStamps];
-};
-__device__ __forceinline__ unsigned long long nw_now() {
-    unsigned long long t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-#define NW_STAMP(st, k)                                 \
-    do {                                                \
-        const unsigned long long now_ = nw_now();       \
-        (st)->acc[k] += now_ - (st)->last;              \
-        (st)->last = now_;                              \
-    } while (0)
-constexpr int kStampsStore = kStamps - 1;
-#else
-struct Stamps {};
-#define NW_STAMP(st, k) ((void)(st))
-#endif
-
-// two adjacent real slots of the half image, one 8/16-byte LDS access
-template <typename T> struct alignas(2 * sizeof(T)) Pair {
-    T a, b;
-};
-
-template <int COMP, typename T> __device__ __forceinline__ T& comp(C2<T>& c) {
-    if constexpr (COMP == 0) return c.re; else return c.im;
-}
-
-// ---- one component of the pass-P outputs -> LDS (P = 0: slots t*E + s, as pairs)
-template <typename T, int N, int E, int P, int COMP>
-__device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
-    using G = Geometry<N, E>;
-    if constexpr (P == 0) {
-        Pair<T>* dst = reinterpret_cast<Pair<T>*>(lds + lds_idx<E>(t * E));
-#pragma unroll
-        for (int u = 0; u < E / 2; ++u)
-            dst[u] = Pair<T>{comp<COMP>(v[bitrev<E>(2 * u)]), comp<COMP>(v[bitrev<E>(2 * u + 1)])};
-    } else {
-        constexpr int R = G::radix(P);
-        constexpr int NS = G::ns(P);
-        constexpr int Q = E / R;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const int j = t + q * G::T;
-            T* dst = lds + lds_idx<E>((j / NS) * NS * R + j % NS);
-#pragma unroll
-            for (int i = 0; i < R; ++i) dst[lds_off<E>(bitrev<R>(i) * NS)] = comp<COMP>(v[q * R + i]);
-        }
-    }
-}
-
-// ---- one component of the pass-P inputs <- LDS.  Butterflies: j = t + q*T, except
-// in the LAST pass, where j = Q*t + q so a thread's outputs come in adjacent pairs.
-template <int N, int E, int P> struct PassInfo {
-    using G = Geometry<N, E>;
-    static constexpr int R = G::radix(P);
-    static constexpr int NS = G::ns(P);
-    static constexpr int Q = E / R;
-    static constexpr int STRIDE = N / R;
-    static constexpr bool LAST = (P == G::npass() - 1);
-    // pairs (j = Q*t + q) only when Q == 2: the two outputs of a lane are then adjacent AND
-    // neighbouring lanes are too (16-B stores, whole lines).  At Q >= 4 pairing put lanes Q
-    // outputs apart (a store instruction touched 1/2 .. 1/4 of each line: 4x slower at
-    // n = 8192); the lane-contiguous j = t + q*T plus DPP packing keeps stores whole.
-    static constexpr bool PAIRED = LAST && Q == 2;
-    static_assert(STRIDE % E == 0 && NS % E == 0, "pad must stay linear");
-    __device__ static __forceinline__ int bfly(int t, int q) { return PAIRED ? Q * t + q : t + q * G::T; }
-};
-
-// Pass-1 twiddles w_{NS*R}^{(j % NS) * r} depend on j % NS only (NS = E, the pass-0
-// radix): an NS x (R-1) table in LDS after the image (7.75 KiB at n = 16384 fp32),
-// filled once per block from the exact global table, replaces that pass's v_sin/v_cos
-// bases and their products (the kernel is power-bound: every VALU op saved counts).
-#ifndef NW_TAB1
-#define NW_TAB1 1
-#endif
-template <typename T, int N, int E> struct Tab1 {
-    using I = PassInfo<N, E, 1>;
-    static constexpr int NS = I::NS, R = I::R;
-    static constexpr int COUNT = Geometry<N, E>::npass() >= 2 ? NS * (R - 1) : 0;
-    static constexpr bool ON = NW_TAB1 && COUNT > 0 && COUNT * (int)sizeof(C2<T>) <= 8192;
-    static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<T>) : 0;
-    static_assert((lds_elems<N, E>() * sizeof(T)) % 16 == 0, "table alignment");
-    __device__ static __forceinline__ const C2<T>* table(const T* lds) {
-        return reinterpret_cast<const C2<T>*>(lds + lds_elems<N, E>());
-    }
-    // w_N^e entries from the exact table tw (tw[i] = exp(+2 pi i / N))
-    __device__ static __forceinline__ void fill(T* lds, const C2<T>* __restrict__ tw, int t) {
-        if constexpr (ON) {
-            C2<T>* tab = reinterpret_cast<C2<T>*>(lds + lds_elems<N, E>());
-            for (int i = t; i < COUNT; i += Geometry<N, E>::T) {
-                const int jj = i % NS, r = i / NS + 1;
-                tab[i] = tw[(jj * r * (N / (NS * R))) % N];
-            }
-        }
-    }
-};
-
-template <typename T, int N, int E, int P, int COMP>
-__device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
-    using I = PassInfo<N, E, P>;
-    constexpr int R = I::R, Q = I::Q;
-    if constexpr (I::PAIRED) {
-        const T* src = lds + lds_idx<E>(Q * t);
-#pragma unroll
-        for (int q = 0; q < Q; q += 2)
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const Pair<T> pr = *reinterpret_cast<const Pair<T>*>(src + q + lds_off<E>(r * I::STRIDE));
-                comp<COMP>(v[q * R + r]) = pr.a;
-                comp<COMP>(v[(q + 1) * R + r]) = pr.b;
-            }
-    } else {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-            const T* src = lds + lds_idx<E>(t + q * Geometry<N, E>::T);
-#pragma unroll
-            for (int r = 0; r < R; ++r) comp<COMP>(v[q * R + r]) = src[lds_off<E>(r * I::STRIDE)];
-        }
-    }
-}
-
-// Workgroup barrier for the LDS image only.  __syncthreads() carries a workgroup
-// release fence that gfx950 lowers to s_waitcnt vmcnt(0): every exchange would
-// wait for ALL of the wave's in-flight global stores.  The exchanges only need
-// this wave's LDS operations complete (lgkmcnt(0)) before the s_barrier.
-__device__ __forceinline__ void lds_barrier() {
-#ifdef NW_FENCED_BARRIER
-    __syncthreads();
-#else
-    __builtin_amdgcn_s_waitcnt(0xC07F);   // vmcnt(63) expcnt(7) lgkmcnt(0): LDS ops only
-    __builtin_amdgcn_s_barrier();
-#endif
-}
-
-// ---- LDS-DMA of the next signal's half spectrum X[0 .. N/2) (N*4 bytes) into the idle
-// LDS image: 16 B per lane per instruction, global_load_lds_dwordx4 writes lane l of
-// a wave at (wave-uniform base) + 16*l.  X[N/2] (the real Nyquist bin) travels by a
-// scalar load.  The DMA is issued before the stores, so the next pass 0 waits for
-// it with vmcnt(#stores issued after it), not for the stores.
-typedef __attribute__((address_space(3))) void lds_void_t;
-typedef __attribute__((address_space(1))) void gbl_void_t;
-
-// LDS-DMA of X[0 .. N/2) (the R2C half spectrum without its Nyquist bin) into LDS at dst:
-// 16 B per lane per instruction, wave w filling its own 1 KiB slices of each round.
-template <typename T, int N, int TT>
-__device__ __forceinline__ void dma_x(const C2<T>* xs, void* dst, int t) {
-    constexpr int CH = (N / 2) * (int)sizeof(C2<T>) / 16;   // 16-byte chunks
-    static_assert(CH % TT == 0, "whole DMA rounds");
-    // wave-uniform LDS destination base in an SGPR (M0 takes it directly; a VGPR copy
-    // per chunk would be hoisted out of the signal loop and spilled)
-    const int wave_base = __builtin_amdgcn_readfirstlane((t & ~63) * 16);
-    const uint32_t lane_off = (uint32_t)t * 16u;
-#pragma unroll
-    for (int i = 0; i < CH / TT; ++i) {
-        // uniform chunk base + opaque 32-bit lane offset: the saddr form, no 64-bit VGPR pairs
-        const char* chunk = reinterpret_cast<const char*>(xs) + (size_t)i * TT * 16;
-        asm volatile("" : "+s"(chunk));           // computed here, in SGPRs (not hoisted)
-        const char* src = at(chunk, lane_off);
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
-                                         (lds_void_t*)(reinterpret_cast<char*>(dst) + i * TT * 16 + wave_base), 16,
-                                         0, 0);
-    }
-}
-
-// s_waitcnt vmcnt(V) with expcnt/lgkmcnt left free (gfx9 encoding: vmcnt[3:0] + [15:14])
-template <int V>
-__device__ __forceinline__ void wait_vmcnt() {
-    static_assert(V >= 0 && V < 64, "vmcnt range");
-    __builtin_amdgcn_s_waitcnt((V & 0xF) | ((V >> 4) << 14) | 0x70 | 0xF00);
-}
-
-// ---- lane-group transposes for the last pass's stores (DPP quad_perm, no LDS)
-template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
-    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
-}
-template <int CTRL> __device__ __forceinline__ double dpp_f(double v) {
-    const long long b = __double_as_longlong(v);
-    const int lo = __builtin_amdgcn_mov_dpp((int)(b & 0xffffffffLL), CTRL, 0xF, 0xF, false);
-    const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
-    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-// 2x2 transpose of (register a, register b) x (lane l, lane l ^ D): the lane with bit D
-// clear keeps a and takes its partner's a as b; the other keeps b and takes the partner's b as a
-template <int D, typename F> __device__ __forceinline__ void xpose2(F& a, F& b, bool hi) {
-    constexpr int CTRL = D == 1 ? 0xB1 : 0x4E;      // quad_perm [1,0,3,2] / [2,3,0,1]
-    const F recv = dpp_f<CTRL>(hi ? a : b);
-    if (hi) a = recv; else b = recv;
-}
-template <typename F> __device__ __forceinline__ void xpose2(C2<F>& a, C2<F>& b, bool hi, int d) {
-    if (d == 1) { xpose2<1>(a.re, b.re, hi); xpose2<1>(a.im, b.im, hi); }
-    else { xpose2<2>(a.re, b.re, hi); xpose2<2>(a.im, b.im, hi); }
-}
-
-// ---- the last pass's outputs: store number i (0 .. nstores-1) of a thread
-// Unpaired last pass (Q = 1: lane t owns outputs t + NS*m, NS apart): PACK lanes swap
-// PACK rows with a PACK x PACK transpose, so each lane stores PACK consecutive outputs
-// as ONE 16-B store -- 4x fewer store instructions for |y|^2 (fp32), 2x for y.  The
-// stores, not their bytes, limited these sizes (n = 4096: 2x the bytes of cwt over
-// power cost +20 % time).
-template <typename T, int N, int E, int OUT>
-struct LastStores {
-    using I = PassInfo<N, E, Geometry<N, E>::npass() - 1>;
-    using O = typename OutT<OUT, T>::type;
-    static constexpr int R = I::R, Q = I::Q;
-    static constexpr int STEP = I::PAIRED ? 2 : 1;
-    static constexpr int PACK_W = (int)(16 / sizeof(O));
-    static constexpr int PACK = (!I::PAIRED && NW_PACK_STORES && PACK_W <= NW_PACK_MAX && R % PACK_W == 0)
-                                    ? PACK_W : 1;
-    static_assert(PACK == 1 || PACK == 2 || PACK == 4, "pack");
-    static constexpr int COUNT = PACK > 1 ? Q * R / PACK : Q / STEP * R;   // store instructions per thread per signal
-    // all stores of one signal (v: the last pass's registers, bit-reversed rows)
-    __device__ static __forceinline__ void all(const C2<T>* v, void* orow, int t) {
-        if constexpr (PACK == 1) {
-            chunk<0, 1>(v, orow, t);
-        } else {
-            const int c = t & (PACK - 1);
-            const uint32_t lane = (uint32_t)((t & ~(PACK - 1)) + I::NS * c) * (uint32_t)sizeof(O);
-#pragma unroll
-            for (int qg = 0; qg < Q * (R / PACK); ++qg) {
-                const int q = qg / (R / PACK), g = qg % (R / PACK);   // butterfly t + q*T, row group g
-                O val[PACK];
-#pragma unroll
-                for (int b = 0; b < PACK; ++b) val[b] = out_value<OUT, T>(v[q * R + bitrev<R>(g * PACK + b)]);
-                if constexpr (PACK >= 2) {
-                    const bool hi1 = c & 1;
-#pragma unroll
-                    for (int b = 0; b < PACK; b += 2) xpose_any<1>(val[b], val[b + 1], hi1);
-                }
-                if constexpr (PACK == 4) {
-                    const bool hi2 = c & 2;
-                    xpose_any<2>(val[0], val[2], hi2);
-                    xpose_any<2>(val[1], val[3], hi2);
-                }
-                using V = float __attribute__((ext_vector_type(4)));
-                struct alignas(16) P16 { O a[PACK]; };
-                P16 pk;
-#pragma unroll
-                for (int b = 0; b < PACK; ++b) pk.a[b] = val[b];
-#ifdef NW_ABL_NOSTORE
-                asm volatile("" ::"v"(__builtin_bit_cast(V, pk)));
-#else
-                __builtin_nontemporal_store(
-                    __builtin_bit_cast(V, pk),
-                    reinterpret_cast<V*>(at(reinterpret_cast<P16*>(orow), lane,
-                                            (uint32_t)((q * Geometry<N, E>::T + g * PACK * I::NS) * sizeof(O)))));
-#endif
-            }
-        }
-    }
-    template <int D, typename F> __device__ static __forceinline__ void xpose_any(F& a, F& b, bool hi) {
-        if constexpr (std::is_same<F, float>::value || std::is_same<F, double>::value) xpose2<D>(a, b, hi);
-        else xpose2(a, b, hi, D);
-    }
-    template <int K>
-    __device__ static __forceinline__ void one(const C2<T>* o, void* orow, int t) {
-        constexpr int q = (K / R) * STEP, i = K % R;
-        const uint32_t lane = (uint32_t)I::bfly(t, 0);        // Q*t (paired) or t
-        constexpr uint32_t c = (uint32_t)((I::PAIRED ? q : q * Geometry<N, E>::T) + bitrev<R>(i) * I::NS);
-        if constexpr (I::PAIRED)
-            store_pair<OUT, T>(orow, lane, c, o[q * R + i], o[(q + 1) * R + i]);
-        else
-            store_one<OUT, T>(orow, lane, c, o[q * R + i]);
-    }
-    // stores [C*COUNT/NCH, (C+1)*COUNT/NCH) -- one chunk of a deferred signal
-    template <int C, int NCH, int K = C * COUNT / NCH>
-    __device__ static __forceinline__ void chunk(const C2<T>* o, void* orow, int t) {
-        if constexpr (K < (C + 1) * COUNT / NCH) {
-            one<K>(o, orow, t);
-            chunk<C, NCH, K + 1>(o, orow, t);
-        }
-    }
-};
-
-
-#ifndef NW_WREG_MAX_E
-#define NW_WREG_MAX_E 16   // W held in registers for the block when E <= this
-#endif
-
-// complex W rows (tables) keep the register path: with LDS-DMA they exceed 128 VGPRs
-template <typename T, int E, bool REALW> constexpr bool kXDMA = sizeof(T) == 4 && E >= NW_XDMA_MIN_E && REALW;
-
-// E = 16 (n <= 8192): X gets its OWN LDS buffer after the image and the pass-1 table, so
-// the next signal's X is DMA'd right after this signal's pass 0 and has the whole signal
-// (exchanges, passes, stores) to land; with W in registers, pass 0 then waits on nothing
-// issued after a store.  (At n = 16384 the 64 KiB buffer would cost a workgroup per CU.)
-#ifndef NW_XBUF
-#define NW_XBUF 0   // measured slower (C3 0.337 -> 0.360 ms): the buffer costs workgroups per CU
-#endif
-template <typename T, int N, int E> struct XBuf {
-    static constexpr bool ON = NW_XBUF && E < 32 && E <= NW_WREG_MAX_E;
-    static constexpr int OFFSET = lds_elems<N, E>() * (int)sizeof(T) + Tab1<T, N, E>::BYTES;
-    static constexpr int BYTES = ON ? (N / 2) * (int)sizeof(C2<T>) : 0;
-    static_assert(OFFSET % 16 == 0, "DMA alignment");
-    __device__ static __forceinline__ C2<T>* at_lds(T* lds) {
-        return reinterpret_cast<C2<T>*>(reinterpret_cast<char*>(lds) + OFFSET);
-    }
-};
-template <typename T, int N, int E> constexpr int kLdsBytes =
-    lds_elems<N, E>() * (int)sizeof(T) + Tab1<T, N, E>::BYTES + XBuf<T, N, E>::BYTES;
-
-
-// ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P.
-// In the last pass (LDS-DMA kernels) the NEXT signal's X is DMA'd into the idle image
-// before this signal's stores are issued: loads, stores and LDS-DMA retire in one
-// in-order vmcnt queue, so the next pass 0 waits for that DMA only.  The last pass
-// stores its outputs straight to HBM.
-template <typename T, int N, int E, int OUT, int P, bool XD>
-__device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>* __restrict__ tw, C2<T>* x,
-                                            const C2<T>* xs_next, void* ocur,
-                                            Stamps* st) {
-    using I = PassInfo<N, E, P>;
-    if constexpr (P < Geometry<N, E>::npass()) {
-        constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
-        constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;
-        C2<T> pb[Q][LR > 0 ? LR : 1];
-#ifndef NW_ABL_NOTWIDDLE
-        if constexpr (!TABLED) {
-#pragma unroll
-            for (int q = 0; q < Q; ++q) twiddle_bases<T, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
-        }
-#endif
-#ifndef NW_ABL_NOEXCH
-        lds_barrier();                         // earlier readers of the image are done
-        if constexpr (P == 1 && XBuf<T, N, E>::ON) {
-            // every wave has read this signal's X: fetch the next one into the buffer
-            if (xs_next) dma_x<T, N, Geometry<N, E>::T>(xs_next, XBuf<T, N, E>::at_lds(lds), t);
-        }
-        lds_write<T, N, E, P - 1, 0>(v, lds, t);
-        lds_barrier();
-        lds_read<T, N, E, P, 0>(v, lds, t);
-        lds_barrier();
-        lds_write<T, N, E, P - 1, 1>(v, lds, t);
-        lds_barrier();
-        lds_read<T, N, E, P, 1>(v, lds, t);
-#else   // ablation (diagnostic builds only): no exchange, the registers stay live
-#pragma unroll
-        for (int i = 0; i < E; ++i) asm volatile("" : "+v"(v[i].re), "+v"(v[i].im));
-#endif
-        if constexpr (I::LAST && XD) {
-            if (xs_next) {                     // the image is idle once every wave has read it
-                lds_barrier();
-                dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        NW_STAMP(st, 2 * P - 1);               // exchange P-1 -> P
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-#ifndef NW_ABL_NOTWIDDLE
-            if constexpr (TABLED) {
-                const C2<T>* tab = Tab1<T, N, E>::table(lds) + I::bfly(t, q) % I::NS;
-#pragma unroll
-                for (int r = 1; r < R; ++r) {
-                    v[q * R + r] = cmul(v[q * R + r], tab[(r - 1) * I::NS]);
-                    if (r % 8 == 7) __builtin_amdgcn_sched_barrier(0);   // <= 8 twiddles in flight
-                }
-            } else {
-                twiddle_apply<T, R>(v + q * R, pb[q]);
-            }
-#endif
-            idft_br<T, R>(v + q * R);
-        }
-        NW_STAMP(st, 2 * P);                   // pass P arithmetic
-        if constexpr (I::LAST) {
-            __builtin_amdgcn_sched_barrier(0);
-            LastStores<T, N, E, OUT>::all(v, ocur, t);
-        } else {
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st);
-        }
-    }
-}
 
 // X[k] at the thread's pass-0 bins k = t + r*T from the R2C half spectrum xs.
 // k < N/2 exactly when r < E/2 (compile-time), so no branch: X[k], or conj(X[N - k])
@@ -1000,6 +367,8 @@ hipError_t prepare_n() {
 }
 
 }  // namespace
+
+hipError_t fused_twiddles(int64_t n, int dtype, void** out) { return twiddles_for(n, dtype, out); }
 
 #ifndef NW_E16384
 #define NW_E16384 32   // elements per thread at n = 16384 fp32 (512 threads)

@@ -1,0 +1,440 @@
+// nw_large.hip — the fused CWT engine for long power-of-two signals (fp32, n = 2^15 .. 2^24).
+//
+// One output row y_f = ifft_n(W_f * X) (reference base.py:378-407: scipy ifft, 1/n folded
+// into W) is longer than one workgroup's LDS holds, so it is computed as a four-step
+// transform n = N1 * N2 (N2 <= 16384 on chip per workgroup, 32 <= N1 <= 1024):
+//
+//   k = k1 + N1*k2,   n = n2 + N2*n1,   Z = W_f * X,   w_M = exp(+2 pi i / M)
+//   y[n2 + N2 n1] = sum_k1 w_N1^(n1 k1) * ( w_n^(n2 k1) * sum_k2 Z[k1 + N1 k2] w_N2^(n2 k2) )
+//
+// Kernels, per signal:
+//   xt_kernel    X (R2C half spectrum, conjugate-mirrored above n/2, interpolate-masked,
+//                base.py:400-401) -> Xt[k1][k2] = X[k1 + N1 k2], n complex; once per signal
+//   rows_kernel  per (scale f, row k1): z[k2] = W_f[k1 + N1 k2] * Xt[k1][k2] with W evaluated
+//                in registers (the expression wtable_kernel uses: analytic psi or the table
+//                row, pad_to + 1/n), pruned to the row's support (kmax[f], the last nonzero
+//                bin), a length-N2 inverse FFT on chip (the nw_fused pass machinery), the
+//                complex row stored to B[f][k1][0 .. N2)
+//   cols_kernel  per (scale f, C consecutive n2): v[k1] = B[f][k1][n2] * w_n^(n2 k1), C
+//                length-N1 inverse FFTs side by side (C * N1 = 16384 points per workgroup,
+//                C * 8 B contiguous per k1 read), epilogue y / |y| / |y|^2 stored to
+//                out[f][n2 + N2 n1] (C * 8 B contiguous runs)
+//
+// HBM per output point: B written and read once (16 B) and y written once; X per row
+// from L2 (rows of one k1 group are swept over 8 scales per XCD tile).  The rocFFT engine
+// it replaces moves K1's product + ~3 in-place passes of rocFFT at n = 2^24.
+#include "nw_fft_dev.h"
+
+namespace nw {
+
+namespace {
+
+constexpr int kRowGroup = 4;      // rows (k1) per rows_kernel workgroup
+constexpr int kRowTileF = 8;      // scales per XCD tile
+constexpr int kRowTileG = 8;      // row groups per XCD tile
+constexpr int kColE = 32;         // elements per thread in cols_kernel
+constexpr int kColThreads = 512;  // cols_kernel workgroup size (C * N1 / kColE)
+constexpr size_t kBBudget = size_t(2) << 30;   // bytes of B per launch pair (scales chunked to fit)
+
+// N2 (on-chip rows) and its elements per thread E: the nw_fused sizes
+template <int N2> constexpr int kRowE = N2 >= 8192 ? 32 : 16;
+
+// ---- X (R2C half spectrum) -> Xt[k1][k2], mirrored + masked (spectrum_bin)
+__global__ __launch_bounds__(256) void xt_kernel(WDesc d, const cplx<float>* __restrict__ X, C2<float>* __restrict__ Xt,
+                                                 int n1, int n2) {
+    __shared__ C2<float> tile[32][33];
+    const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    const int k1_0 = blockIdx.x * 32, k2_0 = blockIdx.y * 32;
+    for (int i = ty; i < 32; i += 8) {
+        const int64_t k = (int64_t)(k1_0 + tx) + (int64_t)n1 * (k2_0 + i);
+        const cplx<float> x = spectrum_bin<float>(X, d, k);
+        tile[i][tx] = C2<float>{x.re, x.im};
+    }
+    __syncthreads();
+    for (int i = ty; i < 32; i += 8) Xt[(int64_t)(k1_0 + i) * n2 + k2_0 + tx] = tile[tx][i];
+}
+
+// ---- kmax[f] = last bin k < min(n, xlim) with W_f[k] != 0 (-1: none); pass-1 pruning
+constexpr int kSupBins = 16;   // bins per thread
+template <bool REALW>
+__global__ __launch_bounds__(256) void kmax_kernel(WDesc d, int* __restrict__ kmax) {
+    const int fi = blockIdx.y;
+    const int64_t lim = d.xlim < d.n ? d.xlim : d.n;
+    const int64_t k0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kSupBins;
+    int m = -1;
+    for (int i = 0; i < kSupBins; ++i) {
+        const int64_t k = k0 + i;
+        if (k >= lim) break;
+        const cplx<float> w = wavelet_bin<float>(d, fi, k);
+        if (w.re != 0.0f || (!REALW && w.im != 0.0f)) m = (int)k;
+    }
+    // wave max, then one atomic per wave
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0 && m >= 0) atomicMax(&kmax[fi], m);
+}
+
+// ---- W_f[k] of one scale in fp32 for a compile-time kind: psi_f32 (nw_internal.h) with
+// the same operations in the same order, times 1/n, as wavelet_bin<float> -- so a row
+// here equals the nw_fused W table bit for bit -- but on 32-bit bin indices (n <= 2^24)
+// and with the per-scale constants hoisted.  j = k - off is the cached row's bin.
+template <int KIND> struct RowW {
+    float xs, b, c1, rr, cpi, sigma, kappa, scale;
+    int off, lenv, jlim;
+    __device__ __forceinline__ void init(const WDesc& d, int fi) {
+        xs = d.xstep32 ? d.xstep32[fi] : 0.0f;
+        b = (float)d.b;
+        c1 = (float)(d.b_over_r * 1.4426950408889634);
+        rr = (float)d.r;
+        cpi = (float)d.cpi;
+        sigma = (float)d.sigma;
+        kappa = (float)d.kappa;
+        scale = (float)d.scale;
+        off = (int)d.off;
+        lenv = d.len_valid < 0x7fffffff ? (int)d.len_valid : 0x7fffffff;
+        if constexpr (KIND == NW_SHANNON) {   // nu = j * delta <= 1.0  <=>  j <= jlim (monotone)
+            int64_t j = (int64_t)(1.0 / d.delta);
+            while ((double)(j + 1) * d.delta <= 1.0) ++j;
+            while (j >= 0 && (double)j * d.delta > 1.0) --j;
+            jlim = j < 0x7fffffff ? (int)j : 0x7fffffff;
+        } else {
+            jlim = 0;
+        }
+    }
+    __device__ __forceinline__ float operator()(int j) const {
+        if ((unsigned)j >= (unsigned)lenv) return 0.0f;
+        float psi;
+        if constexpr (KIND == NW_MORSE) {
+            const float x = (float)j * xs;
+            if (!(x > 0.0f)) return 0.0f;
+            const float lx = __log2f(x);
+            const float e2 = b * lx + c1 * (1.0f - exp2f(rr * lx));
+            psi = 2.0f * exp2f(e2);
+        } else if constexpr (KIND == NW_MORLET) {
+            const float x = (float)j * xs;
+            const float a = sigma - x;
+            psi = cpi * (expf(-(a * a) * 0.5f) - kappa * expf(-(x * x) * 0.5f));
+        } else {
+            psi = j <= jlim ? 1.0f : 0.0f;
+        }
+        return psi * scale;
+    }
+};
+
+// ---- pass 1: rows
+#define NW_LARGE_WPS 4
+template <int N2, int E, int KIND>
+__global__ __launch_bounds__(N2 / E, NW_LARGE_WPS) void rows_kernel(WDesc d, int f0, int nf, int n1,
+                                                                    const C2<float>* __restrict__ Xt,
+                                                                    C2<float>* __restrict__ B,
+                                                                    const int* __restrict__ kmax,
+                                                                    const C2<float>* __restrict__ tw) {
+    using G = Geometry<N2, E>;
+    extern __shared__ __align__(16) unsigned char smem[];
+    float* lds = reinterpret_cast<float*>(smem);
+    const int t = threadIdx.x;
+
+    // XCD-aware block -> (scale, row group), as nw_fused_kernel: blocks b, b+8, ... share
+    // an XCD, whose resident blocks cover kRowTileF scales x kRowTileG row groups, so each
+    // Xt row group is read from HBM once per tile and then from that XCD's L2
+    const int b = blockIdx.x;
+    const int xcd = b & 7;
+    const int local = b >> 3;
+    const int pos = local % (kRowTileF * kRowTileG);
+    const int round = local / (kRowTileF * kRowTileG);
+    const int nfr = (nf + kRowTileF - 1) / kRowTileF;
+    const int fl = (round % nfr) * kRowTileF + pos % kRowTileF;
+    const int rg = ((round / nfr) * kRowTileG + pos / kRowTileF) * 8 + xcd;
+    const int ngroups = n1 / kRowGroup;
+    if (fl >= nf || rg >= ngroups) return;
+    const int fi = f0 + fl;
+    const int km = kmax[fi];
+    RowW<KIND> wf;
+    if constexpr (KIND != NW_TABLE) wf.init(d, fi);
+
+    Tab1<float, N2, E>::fill(lds, tw, t);
+    C2<float> x[E];
+    for (int k1 = rg * kRowGroup; k1 < (rg + 1) * kRowGroup; ++k1) {
+        // bins k = k1 + n1*k2 with k2 = t + r*T: rows r >= need are zero for every thread
+        const int need = km < k1 ? 1 : (km - k1) / n1 / G::T + 1;
+        const C2<float>* xrow = Xt + (int64_t)k1 * N2;
+        const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(C2<float>);
+        C2<float> v[E];
+        auto pass0 = [&]<int NZ>() {
+            int j0 = k1 + n1 * t;                  // bin k of element 0 (k2 = t)
+            if constexpr (KIND != NW_TABLE) j0 -= wf.off;
+            asm volatile("" : "+v"(j0));
+#pragma unroll
+            for (int r = 0; r < E; ++r) {
+                if (r < NZ) {
+                    const C2<float> xv = *at(xrow, xo, (uint32_t)(r * G::T * sizeof(C2<float>)));
+                    const int j = j0 + r * n1 * G::T;
+                    if constexpr (KIND == NW_TABLE) {
+                        const cplx<float> w = wavelet_bin<float>(d, fi, (int64_t)j);
+                        v[r] = cmul(C2<float>{w.re, w.im}, xv);
+                    } else {
+                        const float w = wf(j);
+                        v[r] = C2<float>{w * xv.re, w * xv.im};
+                    }
+                } else {
+                    v[r] = C2<float>{0.0f, 0.0f};
+                }
+            }
+            idft_br<float, E, NZ>(v);
+        };
+        if (need <= 4) pass0.template operator()<4>();
+        else if (need <= 8) pass0.template operator()<8>();
+        else if (E > 16 && need <= 16) pass0.template operator()<(E > 16 ? 16 : E)>();
+        else pass0.template operator()<E>();
+        void* orow = B + ((int64_t)fl * n1 + k1) * N2;
+        passes_from<float, N2, E, NW_OUT_CWT, 1, false>(v, lds, t, tw, x, nullptr, orow, nullptr);
+    }
+}
+
+// ---- pass 2: columns.  Thread t owns column c = t % C of the workgroup's C columns and
+// butterflies u + q*U (U = N1/kColE threads per column).  The exchange image is
+// [position][column] (position-major, C floats per position), one real component at a
+// time: 32-lane groups cover >= 16 consecutive columns, so reads are conflict-free and
+// writes at most 2-way (free for ds_write_b32, MI355X_MICROARCH.md §LDS).
+template <int N1> struct Cols {
+    static constexpr int E = kColE;
+    static constexpr int U = N1 / E;                 // threads per column
+    static constexpr int C = kColThreads / U;        // columns per workgroup
+    using G = Geometry<N1, E>;
+    static_assert(N1 >= 32 && C >= 16, "cols geometry");
+};
+
+template <int N1, int P, int COMP>
+__device__ __forceinline__ void col_write(C2<float>* v, float* lds, int u, int c) {
+    using G = typename Cols<N1>::G;
+    constexpr int C = Cols<N1>::C, U = Cols<N1>::U;
+    constexpr int R = G::radix(P), NS = G::ns(P), Q = kColE / R;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = u + q * U;
+        float* dst = lds + ((j / NS) * NS * R + j % NS) * C + c;
+#pragma unroll
+        for (int i = 0; i < R; ++i) dst[bitrev<R>(i) * NS * C] = comp<COMP>(v[q * R + i]);
+    }
+}
+
+template <int N1, int P, int COMP>
+__device__ __forceinline__ void col_read(C2<float>* v, const float* lds, int u, int c) {
+    using G = typename Cols<N1>::G;
+    constexpr int C = Cols<N1>::C, U = Cols<N1>::U;
+    constexpr int R = G::radix(P), Q = kColE / R, STRIDE = N1 / R;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const float* src = lds + (u + q * U) * C + c;
+#pragma unroll
+        for (int r = 0; r < R; ++r) comp<COMP>(v[q * R + r]) = src[r * STRIDE * C];
+    }
+}
+
+template <int N1, int N2, int OUT, int P>
+__device__ __forceinline__ void col_passes(C2<float>* v, float* lds, int u, int c, void* orow, uint32_t lane_off) {
+    using G = typename Cols<N1>::G;
+    constexpr int U = Cols<N1>::U;
+    constexpr int R = G::radix(P), NS = G::ns(P), Q = kColE / R;
+    if constexpr (P > 0) {
+        constexpr int LR = ilog2<R>();
+        lds_barrier();
+        col_write<N1, P - 1, 0>(v, lds, u, c);
+        lds_barrier();
+        col_read<N1, P, 0>(v, lds, u, c);
+        lds_barrier();
+        col_write<N1, P - 1, 1>(v, lds, u, c);
+        lds_barrier();
+        col_read<N1, P, 1>(v, lds, u, c);
+        // twiddles after the exchange (no stores are in flight here): bases of one
+        // butterfly at a time, so they never sit live across the exchange
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            C2<float> pb[LR > 0 ? LR : 1];
+            twiddle_bases<float, R, N1, NS * R>(pb, (u + q * U) % NS, nullptr);
+            twiddle_apply<float, R>(v + q * R, pb);
+            idft_br<float, R>(v + q * R);
+        }
+    }
+    if constexpr (P + 1 < G::npass()) {
+        col_passes<N1, N2, OUT, P + 1>(v, lds, u, c, orow, lane_off);
+    } else {
+        // v[q*R + i] is y at n1 = (j / NS) * NS * R + j % NS + bitrev(i) * NS, j = u + q*U.
+        // The last pass has N1 / R = NS butterflies, so j < NS and n1 = u + q*U + bitrev(i)*NS:
+        // every store is the lane offset (col + u * N2) plus a compile-time offset
+        using O = typename OutT<OUT, float>::type;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const uint32_t cn1 = (uint32_t)(q * U + bitrev<R>(i) * NS);
+                const O val = out_value<OUT, float>(v[q * R + i]);
+                O* dst = at(reinterpret_cast<O*>(orow), lane_off, cn1 * (uint32_t)N2 * (uint32_t)sizeof(O));
+                if constexpr (OUT == NW_OUT_CWT) {
+                    using V2 = float __attribute__((ext_vector_type(2)));
+                    __builtin_nontemporal_store(__builtin_bit_cast(V2, val), reinterpret_cast<V2*>(dst));
+                } else {
+                    __builtin_nontemporal_store(val, dst);
+                }
+            }
+        }
+    }
+}
+
+template <int N1, int N2, int OUT>
+__global__ __launch_bounds__(kColThreads, 4) void cols_kernel(int f0, int nf, const C2<float>* __restrict__ B,
+                                                              void* __restrict__ out) {
+    using CL = Cols<N1>;
+    constexpr int C = CL::C, U = CL::U, E = kColE;
+    constexpr int64_t n = (int64_t)N1 * N2;
+    extern __shared__ __align__(16) unsigned char smem[];
+    float* lds = reinterpret_cast<float*>(smem);
+    const int t = threadIdx.x;
+    const int c = t % C, u = t / C;
+    constexpr int ngroups = N2 / C;
+    const int fl = blockIdx.x / ngroups;
+    const int cg = blockIdx.x % ngroups;
+    if (fl >= nf) return;
+    const int col = cg * C + c;                      // n2
+    // B[fl] (uniform base) + 32-bit lane offsets: (k1 * N2 + col) * 8 < n * 8 <= 2^27
+    const C2<float>* bf = B + (int64_t)fl * n;
+    const uint32_t boff = ((uint32_t)u * N2 + (uint32_t)col) * (uint32_t)sizeof(C2<float>);
+
+    // pass 0: v[r] = B[k1][n2] * w_n^(n2 k1), k1 = u + U r (radix E, Ns = 1)
+    C2<float> v[E];
+    constexpr float inv_n = 1.0f / (float)n;         // exact: n is a power of two
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int k1 = u + U * r;
+        const C2<float> bv = *at(bf, boff, (uint32_t)(U * r * N2 * sizeof(C2<float>)));
+        const float rev = (float)((uint32_t)col * (uint32_t)k1) * inv_n;   // n2 k1 < n <= 2^24: exact
+        const C2<float> w{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
+        v[r] = cmul(bv, w);
+    }
+    idft_br<float, E>(v);
+    using O = typename OutT<OUT, float>::type;
+    void* orow = reinterpret_cast<char*>(out) + (int64_t)(f0 + fl) * n * (int64_t)sizeof(O);
+    const uint32_t ooff = ((uint32_t)col + (uint32_t)u * N2) * (uint32_t)sizeof(O);
+    col_passes<N1, N2, OUT, 0>(v, lds, u, c, orow, ooff);
+}
+
+template <int N2, int E, int KIND>
+hipError_t launch_row_pass(const WDesc& d, int f0, int nf, int n1, const C2<float>* Xt, C2<float>* B, const int* kmax,
+                       hipStream_t s) {
+    void* tw = nullptr;
+    hipError_t e = fused_twiddles(N2, NW_F32, &tw);
+    if (e != hipSuccess) return e;
+    const int lds = kLdsBytes<float, N2, E>;
+    e = hipFuncSetAttribute((const void*)rows_kernel<N2, E, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    const int ngroups = n1 / kRowGroup;
+    const int gpad = (ngroups + 8 * kRowTileG - 1) / (8 * kRowTileG) * (8 * kRowTileG);
+    const int nfr = (nf + kRowTileF - 1) / kRowTileF;
+    const int64_t blocks = (int64_t)gpad * nfr * kRowTileF;
+    rows_kernel<N2, E, KIND><<<(unsigned)blocks, N2 / E, lds, s>>>(d, f0, nf, n1, Xt, B, kmax,
+                                                                    reinterpret_cast<const C2<float>*>(tw));
+    return hipGetLastError();
+}
+
+template <int N1, int N2>
+hipError_t launch_cols(int out_kind, int f0, int nf, const C2<float>* B, void* out, hipStream_t s) {
+    const int lds = N1 * Cols<N1>::C * (int)sizeof(float);
+    const int64_t blocks = (int64_t)nf * (N2 / Cols<N1>::C);
+    static_assert(N2 % Cols<N1>::C == 0, "column groups");
+    const void* fn = out_kind == NW_OUT_CWT     ? (const void*)cols_kernel<N1, N2, NW_OUT_CWT>
+                     : out_kind == NW_OUT_POWER ? (const void*)cols_kernel<N1, N2, NW_OUT_POWER>
+                                                : (const void*)cols_kernel<N1, N2, NW_OUT_ABS>;
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    if (out_kind == NW_OUT_CWT)
+        cols_kernel<N1, N2, NW_OUT_CWT><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out);
+    else if (out_kind == NW_OUT_POWER)
+        cols_kernel<N1, N2, NW_OUT_POWER><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out);
+    else
+        cols_kernel<N1, N2, NW_OUT_ABS><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out);
+    return hipGetLastError();
+}
+
+// n = N1 * N2: N1 = max(32, n / 16384)
+struct Split {
+    int n1, n2;
+};
+Split split_of(int64_t n) {
+    const int64_t n1 = n / 16384 > 32 ? n / 16384 : 32;
+    return {(int)n1, (int)(n / n1)};
+}
+
+int64_t fchunk_of(int64_t n, int nfreq) {
+    const int64_t per = n * (int64_t)sizeof(C2<float>);
+    int64_t fc = (int64_t)(kBBudget / (size_t)per);
+    if (fc < 1) fc = 1;
+    return fc < nfreq ? fc : nfreq;
+}
+
+}  // namespace
+
+bool large_supported(int64_t n, int dtype) {
+    return dtype == NW_F32 && n >= (int64_t(1) << 15) && n <= (int64_t(1) << 24) && !(n & (n - 1));
+}
+
+size_t large_scratch_bytes(int64_t n, int nfreq) {
+    const size_t per = (size_t)n * sizeof(C2<float>);
+    return per + (size_t)fchunk_of(n, nfreq) * per;   // Xt + B
+}
+
+size_t large_support_bytes(int nfreq) { return (size_t)nfreq * sizeof(int); }
+
+hipError_t build_large_support(const WDesc& d, void* kmax, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(kmax, 0xFF, (size_t)d.nfreq * sizeof(int), s);   // -1
+    if (e != hipSuccess) return e;
+    const int64_t per_block = 256 * kSupBins;
+    dim3 grid((unsigned)((d.n + per_block - 1) / per_block), (unsigned)d.nfreq);
+    if (d.kind == NW_TABLE) kmax_kernel<false><<<grid, 256, 0, s>>>(d, reinterpret_cast<int*>(kmax));
+    else kmax_kernel<true><<<grid, 256, 0, s>>>(d, reinterpret_cast<int*>(kmax));
+    return hipGetLastError();
+}
+
+int64_t large_fchunk(int64_t n, int nfreq) { return fchunk_of(n, nfreq); }
+
+// Xt of one signal (X: its R2C half spectrum) into the scratch's first n complex
+hipError_t large_transpose(const WDesc& d, const void* X, void* scratch, hipStream_t s) {
+    const Split sp = split_of(d.n);
+    xt_kernel<<<dim3((unsigned)(sp.n1 / 32), (unsigned)(sp.n2 / 32)), 256, 0, s>>>(
+        d, reinterpret_cast<const cplx<float>*>(X), reinterpret_cast<C2<float>*>(scratch), sp.n1, sp.n2);
+    return hipGetLastError();
+}
+
+// pass 1 for scales [f0, f0 + nf): Xt -> B (both in the scratch)
+hipError_t large_rows(const WDesc& d, int f0, int nf, const void* kmax, void* scratch, hipStream_t s) {
+    const Split sp = split_of(d.n);
+    C2<float>* Xt = reinterpret_cast<C2<float>*>(scratch);
+    C2<float>* B = Xt + d.n;
+    const int* km = reinterpret_cast<const int*>(kmax);
+#define NW_ROWS(NN)                                                                                \
+    case NN:                                                                                       \
+        switch (d.kind) {                                                                          \
+            case NW_MORSE: return launch_row_pass<NN, kRowE<NN>, NW_MORSE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
+            case NW_MORLET: return launch_row_pass<NN, kRowE<NN>, NW_MORLET>(d, f0, nf, sp.n1, Xt, B, km, s);   \
+            case NW_SHANNON: return launch_row_pass<NN, kRowE<NN>, NW_SHANNON>(d, f0, nf, sp.n1, Xt, B, km, s); \
+            case NW_TABLE: return launch_row_pass<NN, kRowE<NN>, NW_TABLE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
+            default: return hipErrorNotSupported;                                                  \
+        }
+    switch (sp.n2) {
+        NW_ROWS(1024) NW_ROWS(2048) NW_ROWS(4096) NW_ROWS(8192) NW_ROWS(16384)
+        default: return hipErrorNotSupported;
+    }
+#undef NW_ROWS
+}
+
+// pass 2 for scales [f0, f0 + nf): B -> out rows (f, n) of one signal (out: its row 0)
+hipError_t large_cols(const WDesc& d, int out_kind, int f0, int nf, const void* scratch, void* out, hipStream_t s) {
+    const Split sp = split_of(d.n);
+    const C2<float>* B = reinterpret_cast<const C2<float>*>(scratch) + d.n;
+#define NW_COLS(A, BB) \
+    if (sp.n1 == A && sp.n2 == BB) return launch_cols<A, BB>(out_kind, f0, nf, B, out, s);
+    NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(32, 16384)
+    NW_COLS(64, 16384) NW_COLS(128, 16384) NW_COLS(256, 16384) NW_COLS(512, 16384) NW_COLS(1024, 16384)
+    return hipErrorNotSupported;
+#undef NW_COLS
+}
+
+}  // namespace nw

@@ -1,0 +1,120 @@
+"""GPU parity of the two-pass fused engine for long signals (nw_large.hip: fp32,
+power-of-two 2^15 <= n <= 2^24) against the fp64 CPU oracle and the rocFFT engine.
+
+Tolerance (fp32 compute vs the fp64 oracle): max|out - ref| <= 1e-5 * max|ref|
+up to n = 2^16 and 3e-5 above (fp32 FFT round-off grows with log n; the C5 case at 2^24
+keeps 1e-4 in test_gpu_parity.py); |.|^2 outputs twice that.
+"""
+import numpy as np
+import pytest
+
+from oracle import nw_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import ninwavelets_amd as nw  # noqa: E402
+
+CLASSES = {'morse': nw.Morse, 'morlet': nw.Morlet, 'shannon': nw.Shannon, 'mexican_hat': nw.MexicanHat}
+
+
+def rel_err(got, ref):
+    return np.max(np.abs(got - ref)) / max(np.max(np.abs(ref)), 1e-300)
+
+
+def tol(n):
+    return 1e-5 if n <= (1 << 16) else 3e-5
+
+
+def synth(S, n, seed, sfreq=1000.):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / sfreq
+    fc = rng.uniform(1, 100, (S, 1))
+    ph = rng.uniform(0, 2 * np.pi, (S, 1))
+    return (np.sin(2 * np.pi * fc * t + ph) + 0.1 * rng.standard_normal((S, n))).astype(np.float32)
+
+
+def large_ran(w):
+    st = w.plan_stats()
+    return any(s['engine'] == 'fused' and s['launches_rows'] > 0 for s in st)
+
+
+@pytest.mark.parametrize('n', [1 << 15, 1 << 16, 1 << 17, 1 << 18, 1 << 19, 1 << 20, 1 << 21])
+@pytest.mark.parametrize('kind', ['morse', 'morlet', 'shannon'])
+def test_large_cwt_against_oracle(kind, n):
+    """Every N1 x N2 split (N1 = 32 with N2 = 1024 .. 16384, then N2 = 16384 with N1 = 64 ..
+    128) for the analytic kinds; scales from below the bin spacing's reach to 400 Hz."""
+    x = synth(1, n, seed=n % 1000 + len(kind))[0]
+    freqs = np.array([0.5, 3.0, 17.0, 60.0, 250.0, 400.0])
+    w = CLASSES[kind](1000, dtype='float32')
+    got = w.cwt(x, freqs)
+    assert large_ran(w)
+    ref = O.cwt(kind, x.astype(np.float64), freqs)
+    assert got.shape == (freqs.size, n) and got.dtype == np.complex64
+    assert rel_err(got, ref) <= tol(n), rel_err(got, ref)
+
+
+@pytest.mark.parametrize('n', [1 << 16, 1 << 22])
+def test_large_power_abs_and_batch(n):
+    """|.|^2 and |.| from the column pass's epilogue, a batch of signals (one Xt per
+    signal), and the batch equal to the per-signal call."""
+    S = 3 if n <= (1 << 16) else 2
+    x = synth(S, n, seed=7)
+    freqs = np.array([1.0, 8.0, 45.0, 130.0])
+    w = nw.Morse(1000, dtype='float32')
+    c = w.cwt_batch(x, freqs)
+    p = w.cwt_batch(x, freqs, out='power')
+    a = w.cwt_batch(x, freqs, out='abs')
+    assert large_ran(w)
+    assert c.shape == (S, 4, n)
+    for s in range(S):
+        ref = O.cwt('morse', x[s].astype(np.float64), freqs)
+        assert rel_err(c[s], ref) <= 2 * tol(n), (s, rel_err(c[s], ref))
+        assert rel_err(p[s], np.abs(ref) ** 2) <= 4 * tol(n)
+        assert rel_err(a[s], np.abs(ref)) <= 2 * tol(n)
+    assert rel_err(c[S - 1], w.cwt(x[S - 1], freqs)) == 0.0
+
+
+def test_large_interpolate_and_table_kind():
+    """interpolate=True (the X mask and the zero upper half of W, base.py:107-123, 400-401)
+    and a device-built MexicanHat table (complex rows, the NW_TABLE path of the row pass)."""
+    n = 1 << 17
+    x = synth(1, n, seed=11)[0]
+    freqs = np.array([2.0, 20.0, 90.0])
+    w = nw.Morse(1000, dtype='float32', interpolate=True)
+    got = w.cwt(x, freqs)
+    assert large_ran(w)
+    ref = O.cwt('morse', x.astype(np.float64), freqs, interpolate=True)
+    assert rel_err(got, ref) <= tol(n)
+    m = nw.MexicanHat(1000, dtype='float32')
+    got = m.cwt(x, freqs)
+    assert large_ran(m)
+    ref = O.cwt('mexican_hat', x.astype(np.float64), freqs)
+    assert rel_err(got, ref) <= tol(n), rel_err(got, ref)
+
+
+def test_large_engine_agrees_with_rocfft_and_reductions():
+    """The two-pass engine against the rocFFT engine on a 2^20 batch, and the epoch
+    reductions (the fused pass writes |y|^2 per chunk, k_accumulate sums it)."""
+    n = 1 << 20
+    x = synth(2, n, seed=5)
+    freqs = np.linspace(0.5, 250, 12)
+    a = nw.Morse(1000, dtype='float32', engine='rocfft').cwt_batch(x, freqs)
+    w = nw.Morse(1000, dtype='float32')
+    b = w.cwt_batch(x, freqs)
+    assert large_ran(w)
+    assert rel_err(b, a) <= 3e-5, rel_err(b, a)
+    pm = w.cwt_batch(x, freqs, out='power_mean')
+    assert rel_err(pm, np.mean(np.abs(a.astype(np.complex128)) ** 2, axis=0)) <= 1e-4
+
+
+def test_large_support_pruning_edges():
+    """Rows whose support ends inside the first element block (f = 0.1 Hz at 2^18: the
+    Morse row is zero past bin ~ 700) and a scale whose support covers every bin."""
+    n = 1 << 18
+    x = synth(1, n, seed=13)[0]
+    freqs = np.array([0.1, 0.2, 499.0])
+    w = nw.Morse(1000, dtype='float32')
+    got = w.cwt(x, freqs)
+    ref = O.cwt('morse', x.astype(np.float64), freqs)
+    for i in range(freqs.size):
+        assert rel_err(got[i], ref[i]) <= tol(n), (freqs[i], rel_err(got[i], ref[i]))
