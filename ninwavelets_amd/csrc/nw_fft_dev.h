@@ -41,6 +41,17 @@ template <typename T> struct C2 {
     T re, im;
 };
 
+// two fp32 lanes of one VGPR pair: C2<f2> is a PAIR of complex numbers (a.re, b.re),
+// (a.im, b.im) on which every DIF / twiddle template runs as packed math
+// (v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32: two fp32 operations per instruction)
+typedef float f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ C2<f2> pk(C2<float> a, C2<float> b) { return {f2{a.re, b.re}, f2{a.im, b.im}}; }
+__device__ __forceinline__ C2<float> lo(C2<f2> p) { return {p.re.x, p.im.x}; }
+__device__ __forceinline__ C2<float> hi(C2<f2> p) { return {p.re.y, p.im.y}; }
+#ifndef NW_PK
+#define NW_PK 1   // packed fp32 math for pairs of butterflies (Q >= 2 passes)
+#endif
+
 template <typename T> __device__ __forceinline__ C2<T> cmul(C2<T> a, C2<T> b) {
     return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
@@ -631,11 +642,38 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
                     v[q * R + r] = cmul(v[q * R + r], tab[(r - 1) * I::NS]);
                     if (r % 8 == 7) __builtin_amdgcn_sched_barrier(0);   // <= 8 twiddles in flight
                 }
-            } else {
+            } else if constexpr (!(NW_PK && sizeof(T) == 4 && Q % 2 == 0)) {
                 twiddle_apply<T, R>(v + q * R, pb[q]);
             }
 #endif
-            idft_br<T, R>(v + q * R);
+            if constexpr (NW_PK && sizeof(T) == 4 && Q % 2 == 0) {
+                // butterflies q, q+1 as one packed pair: identical DIF networks, per-butterfly
+                // twiddles packed side by side
+                if (q % 2 == 0) {
+                    C2<f2> pv[R];
+#pragma unroll
+                    for (int i = 0; i < R; ++i)
+                        pv[i] = pk(reinterpret_cast<C2<float>*>(v)[q * R + i],
+                                   reinterpret_cast<C2<float>*>(v)[(q + 1) * R + i]);
+#ifndef NW_ABL_NOTWIDDLE
+                    if constexpr (!TABLED) {
+                        C2<f2> pp[LR > 0 ? LR : 1];
+#pragma unroll
+                        for (int k = 0; k < LR; ++k)
+                            pp[k] = pk(reinterpret_cast<C2<float>*>(pb[q])[k], reinterpret_cast<C2<float>*>(pb[q + 1])[k]);
+                        twiddle_apply<f2, R>(pv, pp);
+                    }
+#endif
+                    idft_br<f2, R>(pv);
+#pragma unroll
+                    for (int i = 0; i < R; ++i) {
+                        reinterpret_cast<C2<float>*>(v)[q * R + i] = lo(pv[i]);
+                        reinterpret_cast<C2<float>*>(v)[(q + 1) * R + i] = hi(pv[i]);
+                    }
+                }
+            } else {
+                idft_br<T, R>(v + q * R);
+            }
         }
         NW_STAMP(st, 2 * P);                   // pass P arithmetic
         if constexpr (I::LAST) {

@@ -16,9 +16,14 @@
 //                bin), a length-N2 inverse FFT on chip (the nw_fused pass machinery), the
 //                complex row stored to B[f][k1][0 .. N2)
 //   cols_kernel  per (scale f, C consecutive n2): v[k1] = B[f][k1][n2] * w_n^(n2 k1), C
-//                length-N1 inverse FFTs side by side (C * N1 = 16384 points per workgroup,
-//                C * 8 B contiguous per k1 read), epilogue y / |y| / |y|^2 stored to
-//                out[f][n2 + N2 n1] (C * 8 B contiguous runs)
+//                length-N1 inverse FFTs side by side (C * N1 = 32768 points per 1024-thread
+//                workgroup, C * 8 B contiguous per k1 read), epilogue y / |y| / |y|^2 stored
+//                to out[f][n2 + N2 n1] (C * 8 B = 256-B contiguous runs at N1 = 1024)
+//
+// Measured at C5 (1 x 2^24 x 512, tools/ablate.sh): the column pass is bound by its
+// mixed read + write HBM stream (4.4 TB/s combined; without its stores it reads at
+// 4.7 TB/s and the FFT work costs < 3 %); the row pass is the fused kernel's
+// write-bound form (W evaluation 9 % of it).
 //
 // HBM per output point: B written and read once (16 B) and y written once; X per row
 // from L2 (rows of one k1 group are swept over 8 scales per XCD tile).  The rocFFT engine
@@ -33,7 +38,10 @@ constexpr int kRowGroup = 4;      // rows (k1) per rows_kernel workgroup
 constexpr int kRowTileF = 8;      // scales per XCD tile
 constexpr int kRowTileG = 8;      // row groups per XCD tile
 constexpr int kColE = 32;         // elements per thread in cols_kernel
-constexpr int kColThreads = 512;  // cols_kernel workgroup size (C * N1 / kColE)
+#ifndef NW_COL_THREADS
+#define NW_COL_THREADS 1024   // C = 32 columns at N1 = 1024: 256-B runs; measured C5 cols 1.039 -> 0.978 ms vs 512
+#endif
+constexpr int kColThreads = NW_COL_THREADS;  // cols_kernel workgroup size (C * N1 / kColE)
 constexpr size_t kBBudget = size_t(2) << 30;   // bytes of B per launch pair (scales chunked to fit)
 
 // N2 (on-chip rows) and its elements per thread E: the nw_fused sizes
@@ -172,7 +180,11 @@ __global__ __launch_bounds__(N2 / E, NW_LARGE_WPS) void rows_kernel(WDesc d, int
                         const cplx<float> w = wavelet_bin<float>(d, fi, (int64_t)j);
                         v[r] = cmul(C2<float>{w.re, w.im}, xv);
                     } else {
+#ifdef NW_ABL_ROWS_NOW
+                        const float w = (float)(j & 1);
+#else
                         const float w = wf(j);
+#endif
                         v[r] = C2<float>{w * xv.re, w * xv.im};
                     }
                 } else {
@@ -235,7 +247,11 @@ __device__ __forceinline__ void col_passes(C2<float>* v, float* lds, int u, int 
     using G = typename Cols<N1>::G;
     constexpr int U = Cols<N1>::U;
     constexpr int R = G::radix(P), NS = G::ns(P), Q = kColE / R;
+#ifdef NW_ABL_COLS_NOFFT
+    if constexpr (false) {
+#else
     if constexpr (P > 0) {
+#endif
         constexpr int LR = ilog2<R>();
         lds_barrier();
         col_write<N1, P - 1, 0>(v, lds, u, c);
@@ -269,6 +285,11 @@ __device__ __forceinline__ void col_passes(C2<float>* v, float* lds, int u, int 
                 const uint32_t cn1 = (uint32_t)(q * U + bitrev<R>(i) * NS);
                 const O val = out_value<OUT, float>(v[q * R + i]);
                 O* dst = at(reinterpret_cast<O*>(orow), lane_off, cn1 * (uint32_t)N2 * (uint32_t)sizeof(O));
+#ifdef NW_ABL_COLS_NOSTORE
+                if constexpr (OUT == NW_OUT_CWT) asm volatile("" ::"v"(val.re), "v"(val.im), "v"(dst));
+                else asm volatile("" ::"v"(val), "v"(dst));
+                continue;
+#endif
                 if constexpr (OUT == NW_OUT_CWT) {
                     using V2 = float __attribute__((ext_vector_type(2)));
                     __builtin_nontemporal_store(__builtin_bit_cast(V2, val), reinterpret_cast<V2*>(dst));
@@ -307,10 +328,20 @@ __global__ __launch_bounds__(kColThreads, 4) void cols_kernel(int f0, int nf, co
         const int k1 = u + U * r;
         const C2<float> bv = *at(bf, boff, (uint32_t)(U * r * N2 * sizeof(C2<float>)));
         const float rev = (float)((uint32_t)col * (uint32_t)k1) * inv_n;   // n2 k1 < n <= 2^24: exact
+#ifdef NW_ABL_COLS_NOTW
+        (void)rev;
+        v[r] = bv;
+#else
         const C2<float> w{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
         v[r] = cmul(bv, w);
+#endif
     }
+#ifdef NW_ABL_COLS_NOFFT
+#pragma unroll
+    for (int i = 0; i < E; ++i) asm volatile("" : "+v"(v[i].re), "+v"(v[i].im));
+#else
     idft_br<float, E>(v);
+#endif
     using O = typename OutT<OUT, float>::type;
     void* orow = reinterpret_cast<char*>(out) + (int64_t)(f0 + fl) * n * (int64_t)sizeof(O);
     const uint32_t ooff = ((uint32_t)col + (uint32_t)u * N2) * (uint32_t)sizeof(O);

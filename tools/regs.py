@@ -2,13 +2,14 @@
 """Per-kernel VGPR / scratch / occupancy table of one HIP source (gfx950), from
 clang's -Rpass-analysis=kernel-resource-usage remarks.
     python tools/regs.py ninwavelets_amd/csrc/nw_large.hip [filter]"""
+import os
 import re
 import subprocess
 import sys
 
 src = sys.argv[1]
 flt = sys.argv[2] if len(sys.argv) > 2 else ''
-cmd = ['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++20', '-fno-slp-vectorize',
+cmd = ['/opt/rocm/bin/hipcc', '--offload-arch=gfx950', '-O3', '-std=c++20', '-fno-slp-vectorize', *os.environ.get('DEFS', '').split(),
        '--cuda-device-only', '-c', src, '-o', '/tmp/_regs.co', '-Rpass-analysis=kernel-resource-usage']
 err = subprocess.run(cmd, capture_output=True, text=True, cwd=None).stderr
 rows, cur = [], None
