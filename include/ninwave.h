@@ -57,7 +57,8 @@ extern "C" {
 /* plan flags */
 #define NW_INTERPOLATE   0x1u  /* zero the upper half of fft(x) (interpolate_alias, base.py:400-401) */
 #define NW_ENGINE_ROCFFT 0x10u /* force: rocFFT fwd -> K1 multiply -> rocFFT inv -> K2 epilogue   */
-#define NW_ENGINE_FUSED  0x20u /* force: rocFFT fwd -> fused multiply+LDS inverse FFT+epilogue     */
+#define NW_ENGINE_FUSED  0x20u /* force: rocFFT fwd -> fused multiply+LDS inverse FFT+epilogue
+                                  (n > 16384: the two-pass form, nw_large.hip)                  */
 #define NW_TIMING        0x100u/* record HIP events around every stage (nw_plan_stats)            */
 
 /* execute outputs */
@@ -117,7 +118,9 @@ int nw_device_count(int* n);
  * (base.py:173-194) as called from base.py:238-245. */
 int nw_trans_grid(double real_length, double sfreq, int interpolate, nw_grid* grid);
 
-/* Host-only (no GPU): whether the fused engine supports (n, dtype). */
+/* Host-only (no GPU): whether the fused engine supports (n, dtype): power-of-two n with
+ * 1024 <= n <= 16384 (fp32) / 8192 (fp64) in one on-chip pass, or fp32 2^15 <= n <= 2^24
+ * in its two-pass form (row FFTs of W*X, then column FFTs + epilogue). */
 int nw_fused_supported(int64_t n, int dtype);
 
 /* Create a plan for signals of n samples, up to max_batch signals per device
