@@ -231,14 +231,16 @@ def main():
             out_e = 2 * esz                    # K1 always writes the complex product
         extra = {}
         if two_pass:
-            # column pass (the kernel that writes the output): reads B once (8 B/pt, complex
-            # fp32) and writes each output point once; the row pass writes B once and reads
-            # the transposed spectrum Xt once per launch (from L2 across the scales of a tile)
+            # column pass (the kernel that writes the output): reads B once (2e B/pt, complex
+            # in the compute dtype) and writes each output point once; the row pass writes B
+            # once and reads the transposed spectrum Xt once per launch (from L2 across the
+            # scales of a tile)
+            b_e = 2 * esz
             pts_launch = float(S) * F * n * args.steps / max(1, launches)
-            per_launch = pts_launch * (8 + out_e)
+            per_launch = pts_launch * (b_e + out_e)
             rows_l = max(1, st['launches_rows'])
             rows_pts = float(S) * F * n * args.steps / rows_l
-            rows_bytes = rows_pts * 8 + n * 8
+            rows_bytes = rows_pts * b_e + n * b_e
             rows_ms = st['ms_rows'] / rows_l
             kname = 'cols_kernel'
             extra['roofline_rows'] = {

@@ -276,27 +276,27 @@ int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind
         // epilogue) into the destination rows
         if (!p->wtab_valid) {
             NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes, nw::large_support_bytes(p->nfreq)));
-            NW_HIP(nw::build_large_support(p->desc, p->d_wtab, p->stream));
+            NW_HIP(nw::build_large_support(p->desc, p->dtype, p->d_wtab, p->stream));
             p->wtab_valid = true;
         }
-        NW_TRY(ensure(&p->d_scratch, &p->d_scratch_bytes, nw::large_scratch_bytes(p->n, p->nfreq)));
+        NW_TRY(ensure(&p->d_scratch, &p->d_scratch_bytes, nw::large_scratch_bytes(p->n, p->nfreq, p->dtype)));
         const size_t out_row = (size_t)p->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
-        const int64_t fc = nw::large_fchunk(p->n, p->nfreq);
+        const int64_t fc = nw::large_fchunk(p->n, p->nfreq, p->dtype);
         for (int64_t sidx = 0; sidx < c; ++sidx) {
             const char* Xs = (const char*)p->d_X + (size_t)sidx * p->nh * 2 * p->esz;
             char* os = (char*)dst + (size_t)sidx * p->nfreq * out_row;
             NW_TRY(staged(p, ST_COPY, [&] {   // the spectrum transpose: timed with the copies
-                NW_HIP(nw::large_transpose(p->desc, Xs, p->d_scratch, p->stream));
+                NW_HIP(nw::large_transpose(p->desc, p->dtype, Xs, p->d_scratch, p->stream));
                 return NW_OK;
             }));
             for (int64_t f0 = 0; f0 < p->nfreq; f0 += fc) {
                 const int nf = (int)std::min<int64_t>(fc, p->nfreq - f0);
                 NW_TRY(staged(p, ST_ROWS, [&] {
-                    NW_HIP(nw::large_rows(p->desc, (int)f0, nf, p->d_wtab, p->d_scratch, p->stream));
+                    NW_HIP(nw::large_rows(p->desc, p->dtype, (int)f0, nf, p->d_wtab, p->d_scratch, p->stream));
                     return NW_OK;
                 }));
                 NW_TRY(staged(p, ST_FUSED, [&] {
-                    NW_HIP(nw::large_cols(p->desc, out_kind, (int)f0, nf, p->d_scratch, os, p->stream));
+                    NW_HIP(nw::large_cols(p->desc, p->dtype, out_kind, (int)f0, nf, p->d_wtab, p->d_scratch, os, p->stream));
                     return NW_OK;
                 }));
             }

@@ -127,7 +127,7 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     // before any store is in flight; E = 32: re-read per signal (no VGPRs to spare).
     const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * N;
     const uint32_t wo = (uint32_t)t * (uint32_t)sizeof(WT);
-    constexpr bool WREG = E <= NW_WREG_MAX_E;
+    constexpr bool WREG = E <= NW_WREG_MAX_E && !(sizeof(T) == 8 && N / E > 512);
     WT w[WREG ? E : 1];
     if constexpr (WREG) {
 #pragma unroll
@@ -383,11 +383,11 @@ hipError_t fused_twiddles(int64_t n, int dtype, void** out) { return twiddles_fo
 #define NW_E16384 32   // elements per thread at n = 16384 fp32 (512 threads)
 #endif
 
-// power-of-two n: 2^10..2^14 in fp32, 2^10..2^13 in fp64 (registers: one fp64
-// signal of 16384 points does not fit a 512-thread block's VGPR budget)
+// power-of-two n: 2^10..2^14 (fp64 at 16384: 1024 threads of E = 16 -- one fp64 signal
+// does not fit a 512-thread block's VGPRs -- with W re-read per signal, 128 VGPRs)
 bool fused_supported(int64_t n, int dtype) {
     if (n < 1024 || (n & (n - 1))) return false;
-    return dtype == NW_F32 ? n <= 16384 : (dtype == NW_F64 && n <= 8192);
+    return (dtype == NW_F32 || dtype == NW_F64) && n <= 16384;
 }
 
 #ifndef NW_E4096
@@ -399,7 +399,7 @@ bool fused_supported(int64_t n, int dtype) {
 #define NW_FUSED_TABLE(X)                                                               \
     X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, NW_E4096) X(float, 8192, NW_E8192) \
     X(float, 16384, NW_E16384) X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) \
-    X(double, 8192, 16)
+    X(double, 8192, 16) X(double, 16384, 16)
 
 hipError_t fused_prepare(int64_t n, int dtype) {
 #define NW_PREP(TY, NN, EE) \

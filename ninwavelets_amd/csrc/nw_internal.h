@@ -172,15 +172,17 @@ hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, 
                         int64_t nsig, hipStream_t s);
 hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 pi i j / n), cached per device
 
-// two-pass engine for long signals (nw_large.hip): fp32, power-of-two 2^15 <= n <= 2^24.
-// scratch = Xt (n complex) + B (large_fchunk scales x n complex); kmax = int[nfreq].
+// two-pass engine for long signals (nw_large.hip): power-of-two 2^15 <= n <= 2^24, fp32 or
+// fp64.  scratch = Xt (n complex) + B (large_fchunk scales x n complex); support = kmax[nfreq]
+// + the fp64 column-pass twiddle tables.
 bool       large_supported(int64_t n, int dtype);
-size_t     large_scratch_bytes(int64_t n, int nfreq);
+size_t     large_scratch_bytes(int64_t n, int nfreq, int dtype);
 size_t     large_support_bytes(int nfreq);
-int64_t    large_fchunk(int64_t n, int nfreq);
-hipError_t build_large_support(const WDesc& d, void* kmax, hipStream_t s);
-hipError_t large_transpose(const WDesc& d, const void* X, void* scratch, hipStream_t s);
-hipError_t large_rows(const WDesc& d, int f0, int nf, const void* kmax, void* scratch, hipStream_t s);
-hipError_t large_cols(const WDesc& d, int out_kind, int f0, int nf, const void* scratch, void* out, hipStream_t s);
+int64_t    large_fchunk(int64_t n, int nfreq, int dtype);
+hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStream_t s);
+hipError_t large_transpose(const WDesc& d, int dtype, const void* X, void* scratch, hipStream_t s);
+hipError_t large_rows(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, hipStream_t s);
+hipError_t large_cols(const WDesc& d, int dtype, int out_kind, int f0, int nf, const void* support,
+                      const void* scratch, void* out, hipStream_t s);
 
 }  // namespace nw

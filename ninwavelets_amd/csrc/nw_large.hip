@@ -37,26 +37,29 @@ namespace {
 constexpr int kRowGroup = 4;      // rows (k1) per rows_kernel workgroup
 constexpr int kRowTileF = 8;      // scales per XCD tile
 constexpr int kRowTileG = 8;      // row groups per XCD tile
-constexpr int kColE = 32;         // elements per thread in cols_kernel
 #ifndef NW_COL_THREADS
 #define NW_COL_THREADS 1024   // C = 32 columns at N1 = 1024: 256-B runs; measured C5 cols 1.039 -> 0.978 ms vs 512
 #endif
-constexpr int kColThreads = NW_COL_THREADS;  // cols_kernel workgroup size (C * N1 / kColE)
+constexpr int kColThreads = NW_COL_THREADS;  // cols_kernel workgroup size (C * N1 / E)
 constexpr size_t kBBudget = size_t(2) << 30;   // bytes of B per launch pair (scales chunked to fit)
 
-// N2 (on-chip rows) and its elements per thread E: the nw_fused sizes
-template <int N2> constexpr int kRowE = N2 >= 8192 ? 32 : 16;
+// N2 (on-chip rows) and its elements per thread E: the nw_fused sizes (fp64: E = 16, N2 <= 8192)
+template <typename T, int N2> constexpr int kRowE = sizeof(T) == 4 && N2 >= 8192 ? 32 : 16;
+// elements per thread in cols_kernel: 32 complex fp32 or 16 complex fp64 (64 VGPRs either way)
+template <typename T> constexpr int kColE = sizeof(T) == 4 ? 32 : 16;
+template <typename T> constexpr int kMaxN2 = sizeof(T) == 4 ? 16384 : 8192;
 
 // ---- X (R2C half spectrum) -> Xt[k1][k2], mirrored + masked (spectrum_bin)
-__global__ __launch_bounds__(256) void xt_kernel(WDesc d, const cplx<float>* __restrict__ X, C2<float>* __restrict__ Xt,
+template <typename T>
+__global__ __launch_bounds__(256) void xt_kernel(WDesc d, const cplx<T>* __restrict__ X, C2<T>* __restrict__ Xt,
                                                  int n1, int n2) {
-    __shared__ C2<float> tile[32][33];
+    __shared__ C2<T> tile[32][33];
     const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
     const int k1_0 = blockIdx.x * 32, k2_0 = blockIdx.y * 32;
     for (int i = ty; i < 32; i += 8) {
         const int64_t k = (int64_t)(k1_0 + tx) + (int64_t)n1 * (k2_0 + i);
-        const cplx<float> x = spectrum_bin<float>(X, d, k);
-        tile[i][tx] = C2<float>{x.re, x.im};
+        const cplx<T> x = spectrum_bin<T>(X, d, k);
+        tile[i][tx] = C2<T>{x.re, x.im};
     }
     __syncthreads();
     for (int i = ty; i < 32; i += 8) Xt[(int64_t)(k1_0 + i) * n2 + k2_0 + tx] = tile[tx][i];
@@ -64,7 +67,7 @@ __global__ __launch_bounds__(256) void xt_kernel(WDesc d, const cplx<float>* __r
 
 // ---- kmax[f] = last bin k < min(n, xlim) with W_f[k] != 0 (-1: none); pass-1 pruning
 constexpr int kSupBins = 16;   // bins per thread
-template <bool REALW>
+template <typename T, bool REALW>
 __global__ __launch_bounds__(256) void kmax_kernel(WDesc d, int* __restrict__ kmax) {
     const int fi = blockIdx.y;
     const int64_t lim = d.xlim < d.n ? d.xlim : d.n;
@@ -73,8 +76,8 @@ __global__ __launch_bounds__(256) void kmax_kernel(WDesc d, int* __restrict__ km
     for (int i = 0; i < kSupBins; ++i) {
         const int64_t k = k0 + i;
         if (k >= lim) break;
-        const cplx<float> w = wavelet_bin<float>(d, fi, k);
-        if (w.re != 0.0f || (!REALW && w.im != 0.0f)) m = (int)k;
+        const cplx<T> w = wavelet_bin<T>(d, fi, k);
+        if (w.re != T(0) || (!REALW && w.im != T(0))) m = (int)k;
     }
     // wave max, then one atomic per wave
     for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
@@ -85,7 +88,8 @@ __global__ __launch_bounds__(256) void kmax_kernel(WDesc d, int* __restrict__ km
 // the same operations in the same order, times 1/n, as wavelet_bin<float> -- so a row
 // here equals the nw_fused W table bit for bit -- but on 32-bit bin indices (n <= 2^24)
 // and with the per-scale constants hoisted.  j = k - off is the cached row's bin.
-template <int KIND> struct RowW {
+template <typename T, int KIND> struct RowW;
+template <int KIND> struct RowW<float, KIND> {
     float xs, b, c1, rr, cpi, sigma, kappa, scale;
     int off, lenv, jlim;
     __device__ __forceinline__ void init(const WDesc& d, int fi) {
@@ -128,17 +132,58 @@ template <int KIND> struct RowW {
     }
 };
 
+// fp64: psi_f64 (the reference's expression order: pow / exp on nu = j * delta, nu / f)
+// times 1/n, exactly as wavelet_bin<double>, with the per-scale loads hoisted
+template <int KIND> struct RowW<double, KIND> {
+    double delta, f, peak, b, r, bor, sigma, cpi, kappa, scale;
+    int off, lenv;
+    __device__ __forceinline__ void init(const WDesc& d, int fi) {
+        delta = d.delta;
+        f = d.freq ? d.freq[fi] : 1.0;
+        peak = d.peak ? d.peak[fi] : 1.0;
+        b = d.b;
+        r = d.r;
+        bor = d.b_over_r;
+        sigma = d.sigma;
+        cpi = d.cpi;
+        kappa = d.kappa;
+        scale = d.scale;
+        off = (int)d.off;
+        lenv = d.len_valid < 0x7fffffff ? (int)d.len_valid : 0x7fffffff;
+    }
+    __device__ __forceinline__ double operator()(int j) const {
+        if ((unsigned)j >= (unsigned)lenv) return 0.0;
+        const double nu = (double)(int64_t)j * delta;
+        double psi;
+        if constexpr (KIND == NW_MORSE) {
+            // x^b e^{(b/r)(1 - x^r)} = exp(b ln x + (b/r)(1 - exp(r ln x))): one log and two
+            // exps instead of two pows (relative error ~ |b ln x| eps < 1e-13 over the rows'
+            // support; psi(0) = 0 as np.heaviside(0, 0))
+            const double x = nu / f;
+            if (!(x > 0.0)) return 0.0;
+            const double lx = log(x);
+            psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
+        } else if constexpr (KIND == NW_MORLET) {
+            const double x = nu / f * peak;
+            const double a = sigma - x;
+            psi = cpi * (exp(-(a * a) / 2.0) - kappa * exp(-(x * x) / 2.0));
+        } else {
+            psi = nu <= 1.0 ? 1.0 : 0.0;
+        }
+        return psi * scale;
+    }
+};
+
 // ---- pass 1: rows
 #define NW_LARGE_WPS 4
-template <int N2, int E, int KIND>
-__global__ __launch_bounds__(N2 / E, NW_LARGE_WPS) void rows_kernel(WDesc d, int f0, int nf, int n1,
-                                                                    const C2<float>* __restrict__ Xt,
-                                                                    C2<float>* __restrict__ B,
-                                                                    const int* __restrict__ kmax,
-                                                                    const C2<float>* __restrict__ tw) {
+#define NW_LARGE_WPS64 2   // fp64: twice the registers per element (as nw_fused)
+template <typename T, int N2, int E, int KIND>
+__global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_WPS) void rows_kernel(
+    WDesc d, int f0, int nf, int n1, const C2<T>* __restrict__ Xt, C2<T>* __restrict__ B,
+    const int* __restrict__ kmax, const C2<T>* __restrict__ tw) {
     using G = Geometry<N2, E>;
     extern __shared__ __align__(16) unsigned char smem[];
-    float* lds = reinterpret_cast<float*>(smem);
+    T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
 
     // XCD-aware block -> (scale, row group), as nw_fused_kernel: blocks b, b+8, ... share
@@ -156,17 +201,17 @@ __global__ __launch_bounds__(N2 / E, NW_LARGE_WPS) void rows_kernel(WDesc d, int
     if (fl >= nf || rg >= ngroups) return;
     const int fi = f0 + fl;
     const int km = kmax[fi];
-    RowW<KIND> wf;
+    RowW<T, KIND> wf;
     if constexpr (KIND != NW_TABLE) wf.init(d, fi);
 
-    Tab1<float, N2, E>::fill(lds, tw, t);
-    C2<float> x[E];
+    Tab1<T, N2, E>::fill(lds, tw, t);
+    C2<T> x[E];
     for (int k1 = rg * kRowGroup; k1 < (rg + 1) * kRowGroup; ++k1) {
         // bins k = k1 + n1*k2 with k2 = t + r*T: rows r >= need are zero for every thread
         const int need = km < k1 ? 1 : (km - k1) / n1 / G::T + 1;
-        const C2<float>* xrow = Xt + (int64_t)k1 * N2;
-        const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(C2<float>);
-        C2<float> v[E];
+        const C2<T>* xrow = Xt + (int64_t)k1 * N2;
+        const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(C2<T>);
+        C2<T> v[E];
         auto pass0 = [&]<int NZ>() {
             int j0 = k1 + n1 * t;                  // bin k of element 0 (k2 = t)
             if constexpr (KIND != NW_TABLE) j0 -= wf.off;
@@ -174,79 +219,86 @@ __global__ __launch_bounds__(N2 / E, NW_LARGE_WPS) void rows_kernel(WDesc d, int
 #pragma unroll
             for (int r = 0; r < E; ++r) {
                 if (r < NZ) {
-                    const C2<float> xv = *at(xrow, xo, (uint32_t)(r * G::T * sizeof(C2<float>)));
+                    const C2<T> xv = *at(xrow, xo, (uint32_t)(r * G::T * sizeof(C2<T>)));
                     const int j = j0 + r * n1 * G::T;
                     if constexpr (KIND == NW_TABLE) {
-                        const cplx<float> w = wavelet_bin<float>(d, fi, (int64_t)j);
-                        v[r] = cmul(C2<float>{w.re, w.im}, xv);
+                        const cplx<T> w = wavelet_bin<T>(d, fi, (int64_t)j);
+                        v[r] = cmul(C2<T>{w.re, w.im}, xv);
                     } else {
 #ifdef NW_ABL_ROWS_NOW
-                        const float w = (float)(j & 1);
+                        const T w = (T)(j & 1);
 #else
-                        const float w = wf(j);
+                        const T w = wf(j);
 #endif
-                        v[r] = C2<float>{w * xv.re, w * xv.im};
+                        v[r] = C2<T>{w * xv.re, w * xv.im};
                     }
                 } else {
-                    v[r] = C2<float>{0.0f, 0.0f};
+                    v[r] = C2<T>{T(0), T(0)};
                 }
             }
-            idft_br<float, E, NZ>(v);
+            idft_br<T, E, NZ>(v);
         };
         if (need <= 4) pass0.template operator()<4>();
         else if (need <= 8) pass0.template operator()<8>();
         else if (E > 16 && need <= 16) pass0.template operator()<(E > 16 ? 16 : E)>();
         else pass0.template operator()<E>();
         void* orow = B + ((int64_t)fl * n1 + k1) * N2;
-        passes_from<float, N2, E, NW_OUT_CWT, 1, false>(v, lds, t, tw, x, nullptr, orow, nullptr);
+        passes_from<T, N2, E, NW_OUT_CWT, 1, false>(v, lds, t, tw, x, nullptr, orow, nullptr);
     }
 }
 
 // ---- pass 2: columns.  Thread t owns column c = t % C of the workgroup's C columns and
-// butterflies u + q*U (U = N1/kColE threads per column).  The exchange image is
-// [position][column] (position-major, C floats per position), one real component at a
-// time: 32-lane groups cover >= 16 consecutive columns, so reads are conflict-free and
-// writes at most 2-way (free for ds_write_b32, MI355X_MICROARCH.md §LDS).
-template <int N1> struct Cols {
-    static constexpr int E = kColE;
+// butterflies u + q*U (U = N1/E threads per column).  The exchange image is
+// [position][column] (position-major, C reals per position), one real component at a
+// time: 32-lane groups cover >= 16 consecutive columns (fp32), so reads are conflict-free
+// and writes at most 2-way (free for ds_write_b32, MI355X_MICROARCH.md §LDS); fp64 lanes
+// read 8 B each, so C >= 8 columns keep a 32-lane group on consecutive positions.
+template <typename T, int N1> struct Cols {
+    static constexpr int E = kColE<T>;
     static constexpr int U = N1 / E;                 // threads per column
     static constexpr int C = kColThreads / U;        // columns per workgroup
     using G = Geometry<N1, E>;
-    static_assert(N1 >= 32 && C >= 16, "cols geometry");
+    static_assert(N1 >= 32 && C >= (sizeof(T) == 4 ? 16 : 8), "cols geometry");
 };
 
-template <int N1, int P, int COMP>
-__device__ __forceinline__ void col_write(C2<float>* v, float* lds, int u, int c) {
-    using G = typename Cols<N1>::G;
-    constexpr int C = Cols<N1>::C, U = Cols<N1>::U;
-    constexpr int R = G::radix(P), NS = G::ns(P), Q = kColE / R;
+template <typename T, int N1, int P, int COMP>
+__device__ __forceinline__ void col_write(C2<T>* v, T* lds, int u, int c) {
+    using CL = Cols<T, N1>;
+    using G = typename CL::G;
+    constexpr int C = CL::C, U = CL::U;
+    constexpr int R = G::radix(P), NS = G::ns(P), Q = CL::E / R;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
         const int j = u + q * U;
-        float* dst = lds + ((j / NS) * NS * R + j % NS) * C + c;
+        T* dst = lds + ((j / NS) * NS * R + j % NS) * C + c;
 #pragma unroll
         for (int i = 0; i < R; ++i) dst[bitrev<R>(i) * NS * C] = comp<COMP>(v[q * R + i]);
     }
 }
 
-template <int N1, int P, int COMP>
-__device__ __forceinline__ void col_read(C2<float>* v, const float* lds, int u, int c) {
-    using G = typename Cols<N1>::G;
-    constexpr int C = Cols<N1>::C, U = Cols<N1>::U;
-    constexpr int R = G::radix(P), Q = kColE / R, STRIDE = N1 / R;
+template <typename T, int N1, int P, int COMP>
+__device__ __forceinline__ void col_read(C2<T>* v, const T* lds, int u, int c) {
+    using CL = Cols<T, N1>;
+    using G = typename CL::G;
+    constexpr int C = CL::C, U = CL::U;
+    constexpr int R = G::radix(P), Q = CL::E / R, STRIDE = N1 / R;
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
-        const float* src = lds + (u + q * U) * C + c;
+        const T* src = lds + (u + q * U) * C + c;
 #pragma unroll
         for (int r = 0; r < R; ++r) comp<COMP>(v[q * R + r]) = src[r * STRIDE * C];
     }
 }
 
-template <int N1, int N2, int OUT, int P>
-__device__ __forceinline__ void col_passes(C2<float>* v, float* lds, int u, int c, void* orow, uint32_t lane_off) {
-    using G = typename Cols<N1>::G;
-    constexpr int U = Cols<N1>::U;
-    constexpr int R = G::radix(P), NS = G::ns(P), Q = kColE / R;
+// tw1: fp64 only, the exact length-N1 table exp(+2 pi i j / N1) (fp32 twiddles come from
+// v_sin / v_cos)
+template <typename T, int N1, int N2, int OUT, int P>
+__device__ __forceinline__ void col_passes(C2<T>* v, T* lds, int u, int c, void* orow, uint32_t lane_off,
+                                           const C2<T>* __restrict__ tw1) {
+    using CL = Cols<T, N1>;
+    using G = typename CL::G;
+    constexpr int U = CL::U;
+    constexpr int R = G::radix(P), NS = G::ns(P), Q = CL::E / R;
 #ifdef NW_ABL_COLS_NOFFT
     if constexpr (false) {
 #else
@@ -254,36 +306,36 @@ __device__ __forceinline__ void col_passes(C2<float>* v, float* lds, int u, int 
 #endif
         constexpr int LR = ilog2<R>();
         lds_barrier();
-        col_write<N1, P - 1, 0>(v, lds, u, c);
+        col_write<T, N1, P - 1, 0>(v, lds, u, c);
         lds_barrier();
-        col_read<N1, P, 0>(v, lds, u, c);
+        col_read<T, N1, P, 0>(v, lds, u, c);
         lds_barrier();
-        col_write<N1, P - 1, 1>(v, lds, u, c);
+        col_write<T, N1, P - 1, 1>(v, lds, u, c);
         lds_barrier();
-        col_read<N1, P, 1>(v, lds, u, c);
+        col_read<T, N1, P, 1>(v, lds, u, c);
         // twiddles after the exchange (no stores are in flight here): bases of one
         // butterfly at a time, so they never sit live across the exchange
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            C2<float> pb[LR > 0 ? LR : 1];
-            twiddle_bases<float, R, N1, NS * R>(pb, (u + q * U) % NS, nullptr);
-            twiddle_apply<float, R>(v + q * R, pb);
-            idft_br<float, R>(v + q * R);
+            C2<T> pb[LR > 0 ? LR : 1];
+            twiddle_bases<T, R, N1, NS * R>(pb, (u + q * U) % NS, tw1);
+            twiddle_apply<T, R>(v + q * R, pb);
+            idft_br<T, R>(v + q * R);
         }
     }
     if constexpr (P + 1 < G::npass()) {
-        col_passes<N1, N2, OUT, P + 1>(v, lds, u, c, orow, lane_off);
+        col_passes<T, N1, N2, OUT, P + 1>(v, lds, u, c, orow, lane_off, tw1);
     } else {
         // v[q*R + i] is y at n1 = (j / NS) * NS * R + j % NS + bitrev(i) * NS, j = u + q*U.
         // The last pass has N1 / R = NS butterflies, so j < NS and n1 = u + q*U + bitrev(i)*NS:
         // every store is the lane offset (col + u * N2) plus a compile-time offset
-        using O = typename OutT<OUT, float>::type;
+        using O = typename OutT<OUT, T>::type;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
 #pragma unroll
             for (int i = 0; i < R; ++i) {
                 const uint32_t cn1 = (uint32_t)(q * U + bitrev<R>(i) * NS);
-                const O val = out_value<OUT, float>(v[q * R + i]);
+                const O val = out_value<OUT, T>(v[q * R + i]);
                 O* dst = at(reinterpret_cast<O*>(orow), lane_off, cn1 * (uint32_t)N2 * (uint32_t)sizeof(O));
 #ifdef NW_ABL_COLS_NOSTORE
                 if constexpr (OUT == NW_OUT_CWT) asm volatile("" ::"v"(val.re), "v"(val.im), "v"(dst));
@@ -291,7 +343,7 @@ __device__ __forceinline__ void col_passes(C2<float>* v, float* lds, int u, int 
                 continue;
 #endif
                 if constexpr (OUT == NW_OUT_CWT) {
-                    using V2 = float __attribute__((ext_vector_type(2)));
+                    using V2 = T __attribute__((ext_vector_type(2)));
                     __builtin_nontemporal_store(__builtin_bit_cast(V2, val), reinterpret_cast<V2*>(dst));
                 } else {
                     __builtin_nontemporal_store(val, dst);
@@ -301,14 +353,20 @@ __device__ __forceinline__ void col_passes(C2<float>* v, float* lds, int u, int 
     }
 }
 
-template <int N1, int N2, int OUT>
-__global__ __launch_bounds__(kColThreads, 4) void cols_kernel(int f0, int nf, const C2<float>* __restrict__ B,
-                                                              void* __restrict__ out) {
-    using CL = Cols<N1>;
-    constexpr int C = CL::C, U = CL::U, E = kColE;
+// fp64 pass-0 twiddles w_n^m (m = n2 k1 < n) as the product of two exact entries:
+// tsplit[m & 4095] = w_n^(m mod 4096) and tsplit[4096 + (m >> 12)] = w_n^(4096 (m >> 12))
+constexpr int kSplitLo = 4096;
+constexpr int kSplitEntries = 2 * kSplitLo;   // n <= 2^24: m >> 12 < 4096
+
+template <typename T, int N1, int N2, int OUT>
+__global__ __launch_bounds__(kColThreads, sizeof(T) == 8 ? 2 : 4) void cols_kernel(
+    int f0, int nf, const C2<T>* __restrict__ B, void* __restrict__ out, const C2<T>* __restrict__ tw1,
+    const C2<T>* __restrict__ tsplit) {
+    using CL = Cols<T, N1>;
+    constexpr int C = CL::C, U = CL::U, E = CL::E;
     constexpr int64_t n = (int64_t)N1 * N2;
     extern __shared__ __align__(16) unsigned char smem[];
-    float* lds = reinterpret_cast<float*>(smem);
+    T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
     const int c = t % C, u = t / C;
     constexpr int ngroups = N2 / C;
@@ -316,139 +374,201 @@ __global__ __launch_bounds__(kColThreads, 4) void cols_kernel(int f0, int nf, co
     const int cg = blockIdx.x % ngroups;
     if (fl >= nf) return;
     const int col = cg * C + c;                      // n2
-    // B[fl] (uniform base) + 32-bit lane offsets: (k1 * N2 + col) * 8 < n * 8 <= 2^27
-    const C2<float>* bf = B + (int64_t)fl * n;
-    const uint32_t boff = ((uint32_t)u * N2 + (uint32_t)col) * (uint32_t)sizeof(C2<float>);
+    // B[fl] (uniform base) + 32-bit lane offsets: (k1 * N2 + col) * 16 < n * 16 <= 2^28
+    const C2<T>* bf = B + (int64_t)fl * n;
+    const uint32_t boff = ((uint32_t)u * N2 + (uint32_t)col) * (uint32_t)sizeof(C2<T>);
 
     // pass 0: v[r] = B[k1][n2] * w_n^(n2 k1), k1 = u + U r (radix E, Ns = 1)
-    C2<float> v[E];
-    constexpr float inv_n = 1.0f / (float)n;         // exact: n is a power of two
+    C2<T> v[E];
+    // fp64: w_n^(n2 u) and w_n^(n2 U) from the exact split tables (4 loads per thread), the
+    // E powers by repeated multiplication (<= E ulp of drift, far inside 1e-12)
+    C2<T> wr{T(1), T(0)}, wstep{T(1), T(0)};
+    if constexpr (sizeof(T) == 8) {
+        auto wpow = [&](uint32_t m) {
+            const C2<T> wl = *at(tsplit, (m & (kSplitLo - 1)) * (uint32_t)sizeof(C2<T>));
+            const C2<T> wh = *at(tsplit, (kSplitLo + (m >> 12)) * (uint32_t)sizeof(C2<T>));
+            return cmul(wh, wl);
+        };
+        wr = wpow((uint32_t)col * (uint32_t)u);
+        wstep = wpow((uint32_t)col * (uint32_t)U);
+    }
 #pragma unroll
     for (int r = 0; r < E; ++r) {
         const int k1 = u + U * r;
-        const C2<float> bv = *at(bf, boff, (uint32_t)(U * r * N2 * sizeof(C2<float>)));
-        const float rev = (float)((uint32_t)col * (uint32_t)k1) * inv_n;   // n2 k1 < n <= 2^24: exact
+        const C2<T> bv = *at(bf, boff, (uint32_t)(U * r * N2 * sizeof(C2<T>)));
+        const uint32_t m = (uint32_t)col * (uint32_t)k1;                      // n2 k1 < n <= 2^24
 #ifdef NW_ABL_COLS_NOTW
-        (void)rev;
+        (void)m;
         v[r] = bv;
 #else
-        const C2<float> w{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
-        v[r] = cmul(bv, w);
+        if constexpr (sizeof(T) == 4) {
+            constexpr float inv_n = 1.0f / (float)n;                          // exact: power of two
+            const float rev = (float)m * inv_n;                               // exact: m < 2^24
+            const C2<float> w{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
+            v[r] = cmul(bv, w);
+        } else {
+            (void)m;
+            v[r] = cmul(bv, wr);
+            if (r + 1 < E) wr = cmul(wr, wstep);
+        }
 #endif
     }
 #ifdef NW_ABL_COLS_NOFFT
 #pragma unroll
     for (int i = 0; i < E; ++i) asm volatile("" : "+v"(v[i].re), "+v"(v[i].im));
 #else
-    idft_br<float, E>(v);
+    idft_br<T, E>(v);
 #endif
-    using O = typename OutT<OUT, float>::type;
+    using O = typename OutT<OUT, T>::type;
     void* orow = reinterpret_cast<char*>(out) + (int64_t)(f0 + fl) * n * (int64_t)sizeof(O);
     const uint32_t ooff = ((uint32_t)col + (uint32_t)u * N2) * (uint32_t)sizeof(O);
-    col_passes<N1, N2, OUT, 0>(v, lds, u, c, orow, ooff);
+    col_passes<T, N1, N2, OUT, 0>(v, lds, u, c, orow, ooff, tw1);
 }
 
-template <int N2, int E, int KIND>
-hipError_t launch_row_pass(const WDesc& d, int f0, int nf, int n1, const C2<float>* Xt, C2<float>* B, const int* kmax,
-                       hipStream_t s) {
+// tsplit for one n (fp64 column pass), from sincospi in fp64
+__global__ __launch_bounds__(256) void tsplit_kernel(C2<double>* ts, int64_t n) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= kSplitEntries) return;
+    const int64_t m = i < kSplitLo ? i : (int64_t)(i - kSplitLo) * kSplitLo;
+    double s, c;
+    sincospi(2.0 * (double)(m % n) / (double)n, &s, &c);
+    ts[i] = C2<double>{c, s};
+}
+
+template <typename T, int N2, int E, int KIND>
+hipError_t launch_row_pass(const WDesc& d, int f0, int nf, int n1, const C2<T>* Xt, C2<T>* B, const int* kmax,
+                           hipStream_t s) {
     void* tw = nullptr;
-    hipError_t e = fused_twiddles(N2, NW_F32, &tw);
+    hipError_t e = fused_twiddles(N2, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
-    const int lds = kLdsBytes<float, N2, E>;
-    e = hipFuncSetAttribute((const void*)rows_kernel<N2, E, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    const int lds = kLdsBytes<T, N2, E>;
+    e = hipFuncSetAttribute((const void*)rows_kernel<T, N2, E, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     const int ngroups = n1 / kRowGroup;
     const int gpad = (ngroups + 8 * kRowTileG - 1) / (8 * kRowTileG) * (8 * kRowTileG);
     const int nfr = (nf + kRowTileF - 1) / kRowTileF;
     const int64_t blocks = (int64_t)gpad * nfr * kRowTileF;
-    rows_kernel<N2, E, KIND><<<(unsigned)blocks, N2 / E, lds, s>>>(d, f0, nf, n1, Xt, B, kmax,
-                                                                    reinterpret_cast<const C2<float>*>(tw));
+    rows_kernel<T, N2, E, KIND><<<(unsigned)blocks, N2 / E, lds, s>>>(d, f0, nf, n1, Xt, B, kmax,
+                                                                       reinterpret_cast<const C2<T>*>(tw));
     return hipGetLastError();
 }
 
-template <int N1, int N2>
-hipError_t launch_cols(int out_kind, int f0, int nf, const C2<float>* B, void* out, hipStream_t s) {
-    const int lds = N1 * Cols<N1>::C * (int)sizeof(float);
-    const int64_t blocks = (int64_t)nf * (N2 / Cols<N1>::C);
-    static_assert(N2 % Cols<N1>::C == 0, "column groups");
-    const void* fn = out_kind == NW_OUT_CWT     ? (const void*)cols_kernel<N1, N2, NW_OUT_CWT>
-                     : out_kind == NW_OUT_POWER ? (const void*)cols_kernel<N1, N2, NW_OUT_POWER>
-                                                : (const void*)cols_kernel<N1, N2, NW_OUT_ABS>;
+template <typename T, int N1, int N2>
+hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, const C2<T>* tsplit, hipStream_t s) {
+    using CL = Cols<T, N1>;
+    const int lds = N1 * CL::C * (int)sizeof(T);
+    const int64_t blocks = (int64_t)nf * (N2 / CL::C);
+    static_assert(N2 % CL::C == 0, "column groups");
+    const C2<T>* tw1 = nullptr;
+    if constexpr (sizeof(T) == 8) {
+        void* tw = nullptr;
+        hipError_t e = fused_twiddles(N1, NW_F64, &tw);
+        if (e != hipSuccess) return e;
+        tw1 = reinterpret_cast<const C2<T>*>(tw);
+    }
+    const void* fn = out_kind == NW_OUT_CWT     ? (const void*)cols_kernel<T, N1, N2, NW_OUT_CWT>
+                     : out_kind == NW_OUT_POWER ? (const void*)cols_kernel<T, N1, N2, NW_OUT_POWER>
+                                                : (const void*)cols_kernel<T, N1, N2, NW_OUT_ABS>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     if (out_kind == NW_OUT_CWT)
-        cols_kernel<N1, N2, NW_OUT_CWT><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out);
+        cols_kernel<T, N1, N2, NW_OUT_CWT><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     else if (out_kind == NW_OUT_POWER)
-        cols_kernel<N1, N2, NW_OUT_POWER><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out);
+        cols_kernel<T, N1, N2, NW_OUT_POWER><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     else
-        cols_kernel<N1, N2, NW_OUT_ABS><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out);
+        cols_kernel<T, N1, N2, NW_OUT_ABS><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     return hipGetLastError();
 }
 
-// n = N1 * N2: N1 = max(32, n / 16384)
+// n = N1 * N2: N2 = min(n / 32, 16384 (fp32) or 8192 (fp64)), N1 = n / N2 >= 32
 struct Split {
     int n1, n2;
 };
-Split split_of(int64_t n) {
-    const int64_t n1 = n / 16384 > 32 ? n / 16384 : 32;
+Split split_of(int64_t n, int dtype) {
+    const int64_t maxn2 = dtype == NW_F32 ? kMaxN2<float> : kMaxN2<double>;
+    const int64_t n1 = n / maxn2 > 32 ? n / maxn2 : 32;
     return {(int)n1, (int)(n / n1)};
 }
 
-int64_t fchunk_of(int64_t n, int nfreq) {
-    const int64_t per = n * (int64_t)sizeof(C2<float>);
+size_t cplx_bytes(int dtype) { return dtype == NW_F32 ? sizeof(C2<float>) : sizeof(C2<double>); }
+
+int64_t fchunk_of(int64_t n, int nfreq, int dtype) {
+    const int64_t per = n * (int64_t)cplx_bytes(dtype);
     int64_t fc = (int64_t)(kBBudget / (size_t)per);
     if (fc < 1) fc = 1;
     return fc < nfreq ? fc : nfreq;
 }
 
+// support buffer: kmax[nfreq] (padded to 256 B), then the fp64 split twiddles
+size_t tsplit_offset(int nfreq) { return ((size_t)nfreq * sizeof(int) + 255) / 256 * 256; }
+
 }  // namespace
 
 bool large_supported(int64_t n, int dtype) {
-    return dtype == NW_F32 && n >= (int64_t(1) << 15) && n <= (int64_t(1) << 24) && !(n & (n - 1));
+    return (dtype == NW_F32 || dtype == NW_F64) && n >= (int64_t(1) << 15) && n <= (int64_t(1) << 24) &&
+           !(n & (n - 1));
 }
 
-size_t large_scratch_bytes(int64_t n, int nfreq) {
-    const size_t per = (size_t)n * sizeof(C2<float>);
-    return per + (size_t)fchunk_of(n, nfreq) * per;   // Xt + B
+size_t large_scratch_bytes(int64_t n, int nfreq, int dtype) {
+    const size_t per = (size_t)n * cplx_bytes(dtype);
+    return per + (size_t)fchunk_of(n, nfreq, dtype) * per;   // Xt + B
 }
 
-size_t large_support_bytes(int nfreq) { return (size_t)nfreq * sizeof(int); }
+size_t large_support_bytes(int nfreq) { return tsplit_offset(nfreq) + kSplitEntries * sizeof(C2<double>); }
 
-hipError_t build_large_support(const WDesc& d, void* kmax, hipStream_t s) {
+hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStream_t s) {
+    int* kmax = reinterpret_cast<int*>(support);
     hipError_t e = hipMemsetAsync(kmax, 0xFF, (size_t)d.nfreq * sizeof(int), s);   // -1
     if (e != hipSuccess) return e;
     const int64_t per_block = 256 * kSupBins;
     dim3 grid((unsigned)((d.n + per_block - 1) / per_block), (unsigned)d.nfreq);
-    if (d.kind == NW_TABLE) kmax_kernel<false><<<grid, 256, 0, s>>>(d, reinterpret_cast<int*>(kmax));
-    else kmax_kernel<true><<<grid, 256, 0, s>>>(d, reinterpret_cast<int*>(kmax));
+    const bool realw = d.kind != NW_TABLE;
+    if (dtype == NW_F32) {
+        if (realw) kmax_kernel<float, true><<<grid, 256, 0, s>>>(d, kmax);
+        else kmax_kernel<float, false><<<grid, 256, 0, s>>>(d, kmax);
+    } else {
+        if (realw) kmax_kernel<double, true><<<grid, 256, 0, s>>>(d, kmax);
+        else kmax_kernel<double, false><<<grid, 256, 0, s>>>(d, kmax);
+        tsplit_kernel<<<kSplitEntries / 256, 256, 0, s>>>(
+            reinterpret_cast<C2<double>*>(reinterpret_cast<char*>(support) + tsplit_offset(d.nfreq)), d.n);
+    }
     return hipGetLastError();
 }
 
-int64_t large_fchunk(int64_t n, int nfreq) { return fchunk_of(n, nfreq); }
+int64_t large_fchunk(int64_t n, int nfreq, int dtype) { return fchunk_of(n, nfreq, dtype); }
 
 // Xt of one signal (X: its R2C half spectrum) into the scratch's first n complex
-hipError_t large_transpose(const WDesc& d, const void* X, void* scratch, hipStream_t s) {
-    const Split sp = split_of(d.n);
-    xt_kernel<<<dim3((unsigned)(sp.n1 / 32), (unsigned)(sp.n2 / 32)), 256, 0, s>>>(
-        d, reinterpret_cast<const cplx<float>*>(X), reinterpret_cast<C2<float>*>(scratch), sp.n1, sp.n2);
+hipError_t large_transpose(const WDesc& d, int dtype, const void* X, void* scratch, hipStream_t s) {
+    const Split sp = split_of(d.n, dtype);
+    const dim3 grid((unsigned)(sp.n1 / 32), (unsigned)(sp.n2 / 32));
+    if (dtype == NW_F32)
+        xt_kernel<float><<<grid, 256, 0, s>>>(d, reinterpret_cast<const cplx<float>*>(X),
+                                              reinterpret_cast<C2<float>*>(scratch), sp.n1, sp.n2);
+    else
+        xt_kernel<double><<<grid, 256, 0, s>>>(d, reinterpret_cast<const cplx<double>*>(X),
+                                               reinterpret_cast<C2<double>*>(scratch), sp.n1, sp.n2);
     return hipGetLastError();
 }
 
-// pass 1 for scales [f0, f0 + nf): Xt -> B (both in the scratch)
-hipError_t large_rows(const WDesc& d, int f0, int nf, const void* kmax, void* scratch, hipStream_t s) {
-    const Split sp = split_of(d.n);
-    C2<float>* Xt = reinterpret_cast<C2<float>*>(scratch);
-    C2<float>* B = Xt + d.n;
-    const int* km = reinterpret_cast<const int*>(kmax);
-#define NW_ROWS(NN)                                                                                \
-    case NN:                                                                                       \
-        switch (d.kind) {                                                                          \
-            case NW_MORSE: return launch_row_pass<NN, kRowE<NN>, NW_MORSE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
-            case NW_MORLET: return launch_row_pass<NN, kRowE<NN>, NW_MORLET>(d, f0, nf, sp.n1, Xt, B, km, s);   \
-            case NW_SHANNON: return launch_row_pass<NN, kRowE<NN>, NW_SHANNON>(d, f0, nf, sp.n1, Xt, B, km, s); \
-            case NW_TABLE: return launch_row_pass<NN, kRowE<NN>, NW_TABLE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
-            default: return hipErrorNotSupported;                                                  \
-        }
+namespace {
+template <typename T>
+hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, hipStream_t s) {
+    const Split sp = split_of(d.n, sizeof(T) == 4 ? NW_F32 : NW_F64);
+    C2<T>* Xt = reinterpret_cast<C2<T>*>(scratch);
+    C2<T>* B = Xt + d.n;
+#define NW_ROWS(NN)                                                                                          \
+    case NN:                                                                                                 \
+        if constexpr (NN <= kMaxN2<T>) {                                                                     \
+            constexpr int EE = kRowE<T, NN>;                                                                 \
+            switch (d.kind) {                                                                                \
+                case NW_MORSE: return launch_row_pass<T, NN, EE, NW_MORSE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
+                case NW_MORLET: return launch_row_pass<T, NN, EE, NW_MORLET>(d, f0, nf, sp.n1, Xt, B, km, s);   \
+                case NW_SHANNON: return launch_row_pass<T, NN, EE, NW_SHANNON>(d, f0, nf, sp.n1, Xt, B, km, s); \
+                case NW_TABLE: return launch_row_pass<T, NN, EE, NW_TABLE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
+                default: return hipErrorNotSupported;                                                        \
+            }                                                                                                \
+        }                                                                                                    \
+        return hipErrorNotSupported;
     switch (sp.n2) {
         NW_ROWS(1024) NW_ROWS(2048) NW_ROWS(4096) NW_ROWS(8192) NW_ROWS(16384)
         default: return hipErrorNotSupported;
@@ -456,16 +576,39 @@ hipError_t large_rows(const WDesc& d, int f0, int nf, const void* kmax, void* sc
 #undef NW_ROWS
 }
 
-// pass 2 for scales [f0, f0 + nf): B -> out rows (f, n) of one signal (out: its row 0)
-hipError_t large_cols(const WDesc& d, int out_kind, int f0, int nf, const void* scratch, void* out, hipStream_t s) {
-    const Split sp = split_of(d.n);
-    const C2<float>* B = reinterpret_cast<const C2<float>*>(scratch) + d.n;
+template <typename T>
+hipError_t cols_t(const WDesc& d, int out_kind, int f0, int nf, const void* support, const void* scratch, void* out,
+                  hipStream_t s) {
+    const Split sp = split_of(d.n, sizeof(T) == 4 ? NW_F32 : NW_F64);
+    const C2<T>* B = reinterpret_cast<const C2<T>*>(scratch) + d.n;
+    const C2<T>* ts = sizeof(T) == 8 ? reinterpret_cast<const C2<T>*>(reinterpret_cast<const char*>(support) +
+                                                                      tsplit_offset(d.nfreq))
+                                     : nullptr;
 #define NW_COLS(A, BB) \
-    if (sp.n1 == A && sp.n2 == BB) return launch_cols<A, BB>(out_kind, f0, nf, B, out, s);
-    NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(32, 16384)
-    NW_COLS(64, 16384) NW_COLS(128, 16384) NW_COLS(256, 16384) NW_COLS(512, 16384) NW_COLS(1024, 16384)
+    if (sp.n1 == A && sp.n2 == BB) return launch_cols<T, A, BB>(out_kind, f0, nf, B, out, ts, s);
+    if constexpr (sizeof(T) == 4) {
+        NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(32, 16384)
+        NW_COLS(64, 16384) NW_COLS(128, 16384) NW_COLS(256, 16384) NW_COLS(512, 16384) NW_COLS(1024, 16384)
+    } else {
+        NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(64, 8192)
+        NW_COLS(128, 8192) NW_COLS(256, 8192) NW_COLS(512, 8192) NW_COLS(1024, 8192) NW_COLS(2048, 8192)
+    }
     return hipErrorNotSupported;
 #undef NW_COLS
+}
+}  // namespace
+
+// pass 1 for scales [f0, f0 + nf): Xt -> B (both in the scratch)
+hipError_t large_rows(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, hipStream_t s) {
+    const int* km = reinterpret_cast<const int*>(support);
+    return dtype == NW_F32 ? rows_t<float>(d, f0, nf, km, scratch, s) : rows_t<double>(d, f0, nf, km, scratch, s);
+}
+
+// pass 2 for scales [f0, f0 + nf): B -> out rows (f, n) of one signal (out: its row 0)
+hipError_t large_cols(const WDesc& d, int dtype, int out_kind, int f0, int nf, const void* support,
+                      const void* scratch, void* out, hipStream_t s) {
+    return dtype == NW_F32 ? cols_t<float>(d, out_kind, f0, nf, support, scratch, out, s)
+                           : cols_t<double>(d, out_kind, f0, nf, support, scratch, out, s);
 }
 
 }  // namespace nw

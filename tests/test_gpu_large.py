@@ -1,9 +1,10 @@
-"""GPU parity of the two-pass fused engine for long signals (nw_large.hip: fp32,
+"""GPU parity of the two-pass fused engine for long signals (nw_large.hip: fp32 and fp64,
 power-of-two 2^15 <= n <= 2^24) against the fp64 CPU oracle and the rocFFT engine.
 
 Tolerance (fp32 compute vs the fp64 oracle): max|out - ref| <= 1e-5 * max|ref|
 up to n = 2^16 and 3e-5 above (fp32 FFT round-off grows with log n; the C5 case at 2^24
-keeps 1e-4 in test_gpu_parity.py); |.|^2 outputs twice that.
+keeps 1e-4 in test_gpu_parity.py); |.|^2 outputs twice that.  fp64 compute: 1e-12 (as every
+fp64 parity test), |.|^2 2e-12.
 """
 import numpy as np
 import pytest
@@ -118,3 +119,63 @@ def test_large_support_pruning_edges():
     ref = O.cwt('morse', x.astype(np.float64), freqs)
     for i in range(freqs.size):
         assert rel_err(got[i], ref[i]) <= tol(n), (freqs[i], rel_err(got[i], ref[i]))
+
+
+# ------------------------------------------------------------------ fp64 (the reference's dtype)
+@pytest.mark.parametrize('n', [1 << 15, 1 << 16, 1 << 18, 1 << 19, 1 << 21])
+@pytest.mark.parametrize('kind', ['morse', 'morlet', 'shannon'])
+def test_large_fp64_against_oracle(kind, n):
+    """The fp64 two-pass form (N2 <= 8192 on chip, N1 = 32 .. 256 here; pass-0 column
+    twiddles from two exact tables) for the analytic kinds at the default compute dtype."""
+    x = synth(1, n, seed=n % 997 + len(kind))[0].astype(np.float64)
+    freqs = np.array([0.5, 3.0, 17.0, 60.0, 250.0, 400.0])
+    w = CLASSES[kind](1000)
+    got = w.cwt(x, freqs)
+    assert large_ran(w)
+    ref = O.cwt(kind, x, freqs)
+    assert got.shape == (freqs.size, n) and got.dtype == np.complex128
+    assert rel_err(got, ref) <= 1e-12, rel_err(got, ref)
+
+
+def test_large_fp64_outputs_batch_table_and_rocfft_agreement():
+    """fp64: |.|^2 / |.| epilogues, a 2-signal batch, interpolate, a MexicanHat table (complex
+    rows) and agreement with the rocFFT engine."""
+    n = 1 << 17
+    x = synth(2, n, seed=17).astype(np.float64)
+    freqs = np.array([1.0, 8.0, 45.0, 130.0])
+    w = nw.Morse(1000)
+    c = w.cwt_batch(x, freqs)
+    p = w.cwt_batch(x, freqs, out='power')
+    a = w.cwt_batch(x, freqs, out='abs')
+    assert large_ran(w)
+    for s in range(2):
+        ref = O.cwt('morse', x[s], freqs)
+        assert rel_err(c[s], ref) <= 1e-12
+        assert rel_err(p[s], np.abs(ref) ** 2) <= 2e-12
+        assert rel_err(a[s], np.abs(ref)) <= 1e-12
+    r = nw.Morse(1000, engine='rocfft').cwt_batch(x, freqs)
+    assert rel_err(c, r) <= 1e-12
+    wi = nw.Morse(1000, interpolate=True)
+    assert rel_err(wi.cwt(x[0], freqs), O.cwt('morse', x[0], freqs, interpolate=True)) <= 1e-12
+    assert large_ran(wi)
+    m = nw.MexicanHat(1000)
+    assert rel_err(m.cwt(x[1], freqs), O.cwt('mexican_hat', x[1], freqs)) <= 1e-12
+    assert large_ran(m)
+
+
+@pytest.mark.parametrize('out', ['cwt', 'power', 'abs'])
+@pytest.mark.parametrize('kind', ['morse', 'mexican_hat'])
+def test_fused_fp64_16384_one_pass(kind, out):
+    """fp64 at n = 16384: the one-pass fused kernel with 1024 threads (E = 16, W re-read
+    per signal), real (Morse) and complex (MexicanHat table) rows, against the oracle."""
+    n, S = 16384, 3
+    x = synth(S, n, seed=29).astype(np.float64)
+    freqs = np.array([0.7, 5.0, 33.0, 260.0])
+    w = CLASSES[kind](1000)
+    got = w.cwt_batch(x, freqs, out=out)
+    st = w.plan_stats()
+    assert any(s['engine'] == 'fused' and s['launches_fused'] > 0 and s['launches_rows'] == 0 for s in st)
+    for s in range(S):
+        ref = O.cwt(kind, x[s], freqs)
+        ref = {'cwt': ref, 'power': np.abs(ref) ** 2, 'abs': np.abs(ref)}[out]
+        assert rel_err(got[s], ref) <= (2e-12 if out == 'power' else 1e-12), (s, rel_err(got[s], ref))

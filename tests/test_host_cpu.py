@@ -74,6 +74,11 @@ def test_trans_grid_rejects_bad_args():
 
 def test_fused_support_table():
     assert L.fused_supported(300, L.NW_F32) is False        # non power of two -> rocFFT engine
+    assert L.fused_supported(512, L.NW_F64) is False        # below the smallest on-chip size
+    for dt in (L.NW_F32, L.NW_F64):
+        for lg in range(10, 25):                             # one pass to 2^14, two passes above
+            assert L.fused_supported(1 << lg, dt) is True, (lg, dt)
+        assert L.fused_supported(1 << 25, dt) is False
 
 
 # ---------------------------------------------------------------- host-side errors
