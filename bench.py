@@ -63,16 +63,20 @@ def synth_device(torch, S, n, seed, device, sfreq=1000., dtype=None):
     return x
 
 
-def pmc_traffic(kernel, config, chunk, engine):
+def pmc_traffic(kernel, config, chunk, engine, dtype='float32', out=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    same bench command (tools/gpu_round.sh -> profiles/pmc_<config>_<engine>.json), or None."""
+    same bench command (tools/gpu_round.sh -> profiles/pmc_<config>_<engine>.json), or None
+    when the summary was taken on another kernel, chunk, dtype or output kind."""
     path = os.path.join(ROOT, 'profiles', f'pmc_{config}_{engine}.json')
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    if d.get('kernel') != kernel or d.get('config', {}).get('chunk') != chunk:
+    c = d.get('config', {})
+    if d.get('kernel') != kernel or c.get('chunk') != chunk or c.get('dtype', 'float32') != dtype:
+        return None
+    if out is not None and c.get('out', out) != out:
         return None
     return d.get('hbm_bytes_per_launch')
 
@@ -261,7 +265,7 @@ def main():
         roof = {'kernel': kname, 'bound': 'hbm',
                 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
                 'frac': round(achieved / PEAK_HBM_GBPS, 4),
-                'traffic': pmc_traffic(kname, args.config, C, st['engine']),
+                'traffic': pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind),
                 'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
         stage_ms = {k: round(st[k] / args.steps, 3) for k in
                     ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_rows', 'ms_copy')}

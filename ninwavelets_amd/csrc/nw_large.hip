@@ -28,13 +28,20 @@
 // HBM per output point: B written and read once (16 B) and y written once; X per row
 // from L2 (rows of one k1 group are swept over 8 scales per XCD tile).  The rocFFT engine
 // it replaces moves K1's product + ~3 in-place passes of rocFFT at n = 2^24.
+// B is written with streaming (nt) stores like every output: measured at C5, plain stores
+// (to keep B in the 256 MiB Infinity Cache for the column pass) and 1-2 scales per launch
+// pair (B = 134-268 MB) were slower (51.6 / 65.1 / 93.2 ms per step for 16 / 2 / 1 scales
+// with plain stores vs 49.3 with nt at 16): the column pass gains <= 8 % from the cache
+// hits, the row pass loses its Xt reuse across the scales of a tile.
+#include <cstdlib>
+
 #include "nw_fft_dev.h"
 
 namespace nw {
 
 namespace {
 
-constexpr int kRowGroup = 4;      // rows (k1) per rows_kernel workgroup
+constexpr int kRowGroup = 4;      // rows (k1) per rows_kernel workgroup (1 when a launch holds few scales)
 constexpr int kRowTileF = 8;      // scales per XCD tile
 constexpr int kRowTileG = 8;      // row groups per XCD tile
 #ifndef NW_COL_THREADS
@@ -179,7 +186,7 @@ template <int KIND> struct RowW<double, KIND> {
 #define NW_LARGE_WPS64 2   // fp64: twice the registers per element (as nw_fused)
 template <typename T, int N2, int E, int KIND>
 __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_WPS) void rows_kernel(
-    WDesc d, int f0, int nf, int n1, const C2<T>* __restrict__ Xt, C2<T>* __restrict__ B,
+    WDesc d, int f0, int nf, int n1, int rgs, const C2<T>* __restrict__ Xt, C2<T>* __restrict__ B,
     const int* __restrict__ kmax, const C2<T>* __restrict__ tw) {
     using G = Geometry<N2, E>;
     extern __shared__ __align__(16) unsigned char smem[];
@@ -197,7 +204,7 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_
     const int nfr = (nf + kRowTileF - 1) / kRowTileF;
     const int fl = (round % nfr) * kRowTileF + pos % kRowTileF;
     const int rg = ((round / nfr) * kRowTileG + pos / kRowTileF) * 8 + xcd;
-    const int ngroups = n1 / kRowGroup;
+    const int ngroups = n1 / rgs;
     if (fl >= nf || rg >= ngroups) return;
     const int fi = f0 + fl;
     const int km = kmax[fi];
@@ -206,7 +213,7 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_
 
     Tab1<T, N2, E>::fill(lds, tw, t);
     C2<T> x[E];
-    for (int k1 = rg * kRowGroup; k1 < (rg + 1) * kRowGroup; ++k1) {
+    for (int k1 = rg * rgs; k1 < (rg + 1) * rgs; ++k1) {
         // bins k = k1 + n1*k2 with k2 = t + r*T: rows r >= need are zero for every thread
         const int need = km < k1 ? 1 : (km - k1) / n1 / G::T + 1;
         const C2<T>* xrow = Xt + (int64_t)k1 * N2;
@@ -444,11 +451,12 @@ hipError_t launch_row_pass(const WDesc& d, int f0, int nf, int n1, const C2<T>* 
     const int lds = kLdsBytes<T, N2, E>;
     e = hipFuncSetAttribute((const void*)rows_kernel<T, N2, E, KIND>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    const int ngroups = n1 / kRowGroup;
+    const int rgs = nf < kRowTileF ? 1 : kRowGroup;   // few scales: one row per block, more blocks
+    const int ngroups = n1 / rgs;
     const int gpad = (ngroups + 8 * kRowTileG - 1) / (8 * kRowTileG) * (8 * kRowTileG);
     const int nfr = (nf + kRowTileF - 1) / kRowTileF;
     const int64_t blocks = (int64_t)gpad * nfr * kRowTileF;
-    rows_kernel<T, N2, E, KIND><<<(unsigned)blocks, N2 / E, lds, s>>>(d, f0, nf, n1, Xt, B, kmax,
+    rows_kernel<T, N2, E, KIND><<<(unsigned)blocks, N2 / E, lds, s>>>(d, f0, nf, n1, rgs, Xt, B, kmax,
                                                                        reinterpret_cast<const C2<T>*>(tw));
     return hipGetLastError();
 }
@@ -495,6 +503,7 @@ size_t cplx_bytes(int dtype) { return dtype == NW_F32 ? sizeof(C2<float>) : size
 int64_t fchunk_of(int64_t n, int nfreq, int dtype) {
     const int64_t per = n * (int64_t)cplx_bytes(dtype);
     int64_t fc = (int64_t)(kBBudget / (size_t)per);
+    if (const char* e = std::getenv("NW_LARGE_FCHUNK")) fc = std::atoll(e);   // diagnostics
     if (fc < 1) fc = 1;
     return fc < nfreq ? fc : nfreq;
 }
