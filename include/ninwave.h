@@ -119,8 +119,8 @@ int nw_device_count(int* n);
 int nw_trans_grid(double real_length, double sfreq, int interpolate, nw_grid* grid);
 
 /* Host-only (no GPU): whether the fused engine supports (n, dtype): power-of-two n with
- * 1024 <= n <= 16384 (fp32) / 8192 (fp64) in one on-chip pass, or fp32 2^15 <= n <= 2^24
- * in its two-pass form (row FFTs of W*X, then column FFTs + epilogue). */
+ * 1024 <= n <= 16384 in one on-chip pass, or 2^15 <= n <= 2^24 in its two-pass form (row
+ * FFTs of W*X, then column FFTs + epilogue); fp32 and fp64 alike. */
 int nw_fused_supported(int64_t n, int dtype);
 
 /* Create a plan for signals of n samples, up to max_batch signals per device
