@@ -25,6 +25,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+DEFAULT_CHUNK = {'c4': 512, 'c3': 1024, 'c2': 64, 'c5': 1}   # signals per fused launch (tools/chunk_sweep.sh)
 PEAK_HBM_GBPS = 8000.0     # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 
 CONFIGS = {
@@ -143,7 +144,9 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='c4', choices=sorted(CONFIGS))
     ap.add_argument('--engine', default='auto', choices=['auto', 'rocfft', 'fused'])
-    ap.add_argument('--chunk', type=int, default=256, help='signals per device chunk')
+    ap.add_argument('--chunk', type=int, default=None,
+                    help='signals per device chunk (default per config: c4 512, c3 1024; measured '
+                         'vs 256: +1 %% / +7 %% from fewer launch gaps and forward-FFT launches)')
     ap.add_argument('--epochs', type=int, default=None, help='override epochs per GPU')
     ap.add_argument('--output', default=None, choices=['cwt', 'abs', 'power'],
                     help='override the config\'s output kind (diagnostics)')
@@ -178,7 +181,7 @@ def main():
         dtype = args.dtype
     S = epochs * chans                       # signals on this rank
     F = len(freqs)
-    C = min(args.chunk, S)
+    C = min(args.chunk or DEFAULT_CHUNK.get(args.config, 256), S)
     f64 = dtype == 'float64'
     x = synth_device(torch, S, n, seed=1000 + rank, device=dev, dtype=torch.float64 if f64 else torch.float32)
     odt = {('cwt', False): torch.complex64, ('cwt', True): torch.complex128}.get(
