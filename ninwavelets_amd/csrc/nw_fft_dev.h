@@ -338,7 +338,9 @@ __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
 
 // ---- one component of the pass-P inputs <- LDS.  Butterflies: j = t + q*T, except
 // in the LAST pass, where j = Q*t + q so a thread's outputs come in adjacent pairs.
-template <int N, int E, int P> struct PassInfo {
+// OSZ: bytes of one output value (pairing is only worth it for outputs <= 8 B: a pair of
+// 16-B complex128 outputs is two 16-B stores per lane, each touching every other 16 B)
+template <int N, int E, int P, int OSZ = 8> struct PassInfo {
     using G = Geometry<N, E>;
     static constexpr int R = G::radix(P);
     static constexpr int NS = G::ns(P);
@@ -349,7 +351,7 @@ template <int N, int E, int P> struct PassInfo {
     // neighbouring lanes are too (16-B stores, whole lines).  At Q >= 4 pairing put lanes Q
     // outputs apart (a store instruction touched 1/2 .. 1/4 of each line: 4x slower at
     // n = 8192); the lane-contiguous j = t + q*T plus DPP packing keeps stores whole.
-    static constexpr bool PAIRED = LAST && Q == 2;
+    static constexpr bool PAIRED = LAST && Q == 2 && OSZ <= 8;
     static_assert(STRIDE % E == 0 && NS % E == 0, "pad must stay linear");
     __device__ static __forceinline__ int bfly(int t, int q) { return PAIRED ? Q * t + q : t + q * G::T; }
 };
@@ -383,9 +385,9 @@ template <typename T, int N, int E> struct Tab1 {
     }
 };
 
-template <typename T, int N, int E, int P, int COMP>
+template <typename T, int N, int E, int P, int COMP, int OSZ>
 __device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
-    using I = PassInfo<N, E, P>;
+    using I = PassInfo<N, E, P, OSZ>;
     constexpr int R = I::R, Q = I::Q;
     if constexpr (I::PAIRED) {
         const T* src = lds + lds_idx<E>(Q * t);
@@ -487,8 +489,8 @@ template <typename F> __device__ __forceinline__ void xpose2(C2<F>& a, C2<F>& b,
 // power cost +20 % time).
 template <typename T, int N, int E, int OUT>
 struct LastStores {
-    using I = PassInfo<N, E, Geometry<N, E>::npass() - 1>;
     using O = typename OutT<OUT, T>::type;
+    using I = PassInfo<N, E, Geometry<N, E>::npass() - 1, (int)sizeof(O)>;
     static constexpr int R = I::R, Q = I::Q;
     static constexpr int STEP = I::PAIRED ? 2 : 1;
     static constexpr int PACK_W = (int)(16 / sizeof(O));
@@ -596,7 +598,8 @@ template <typename T, int N, int E, int OUT, int P, bool XD>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
                                             Stamps* st) {
-    using I = PassInfo<N, E, P>;
+    constexpr int OSZ = (int)sizeof(typename OutT<OUT, T>::type);
+    using I = PassInfo<N, E, P, OSZ>;
     if constexpr (P < Geometry<N, E>::npass()) {
         constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
         constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;
@@ -615,11 +618,11 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
         }
         lds_write<T, N, E, P - 1, 0>(v, lds, t);
         lds_barrier();
-        lds_read<T, N, E, P, 0>(v, lds, t);
+        lds_read<T, N, E, P, 0, OSZ>(v, lds, t);
         lds_barrier();
         lds_write<T, N, E, P - 1, 1>(v, lds, t);
         lds_barrier();
-        lds_read<T, N, E, P, 1>(v, lds, t);
+        lds_read<T, N, E, P, 1, OSZ>(v, lds, t);
 #else   // ablation (diagnostic builds only): no exchange, the registers stay live
 #pragma unroll
         for (int i = 0; i < E; ++i) asm volatile("" : "+v"(v[i].re), "+v"(v[i].im));
