@@ -383,8 +383,8 @@ hipError_t fused_twiddles(int64_t n, int dtype, void** out) { return twiddles_fo
 #define NW_E16384 32   // elements per thread at n = 16384 fp32 (512 threads)
 #endif
 
-// power-of-two n: 2^10..2^14 (fp64 at 16384: 1024 threads of E = 16 -- one fp64 signal
-// does not fit a 512-thread block's VGPRs -- with W re-read per signal, 128 VGPRs)
+// power-of-two n: 2^10..2^14 in fp32 and fp64 (fp64 at 8192 / 16384: E = 32 with 256 VGPRs,
+// W re-read per signal)
 bool fused_supported(int64_t n, int dtype) {
     if (n < 1024 || (n & (n - 1))) return false;
     return (dtype == NW_F32 || dtype == NW_F64) && n <= 16384;
@@ -396,10 +396,20 @@ bool fused_supported(int64_t n, int dtype) {
 #ifndef NW_E8192
 #define NW_E8192 32   // measured: n = 8192 power 0.887 -> 0.768 ms, cwt 1.034 -> 0.926 ms vs E = 16
 #endif
+// fp64 at n >= 8192: E = 32 (3 passes, 256 VGPRs, 2 waves/SIMD, 2 blocks per CU at 8192)
+// instead of E = 16 (4 passes: 16-16-16-2/4, one 512-thread block per CU at 8192).
+// Measured (256 signals x 256 scales): 8192 cwt 2.907 -> 2.573 ms, power 2.397 -> 1.991;
+// 16384 (128 signals) cwt 3.447 -> 3.124, power 2.615 -> 2.312.
+#ifndef NW_E8192_64
+#define NW_E8192_64 32
+#endif
+#ifndef NW_E16384_64
+#define NW_E16384_64 32
+#endif
 #define NW_FUSED_TABLE(X)                                                               \
     X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, NW_E4096) X(float, 8192, NW_E8192) \
     X(float, 16384, NW_E16384) X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) \
-    X(double, 8192, 16) X(double, 16384, 16)
+    X(double, 8192, NW_E8192_64) X(double, 16384, NW_E16384_64)
 
 hipError_t fused_prepare(int64_t n, int dtype) {
 #define NW_PREP(TY, NN, EE) \

@@ -51,7 +51,12 @@ constexpr int kColThreads = NW_COL_THREADS;  // cols_kernel workgroup size (C * 
 constexpr size_t kBBudget = size_t(2) << 30;   // bytes of B per launch pair (scales chunked to fit)
 
 // N2 (on-chip rows) and its elements per thread E: the nw_fused sizes (fp64: E = 16, N2 <= 8192)
-template <typename T, int N2> constexpr int kRowE = sizeof(T) == 4 && N2 >= 8192 ? 32 : 16;
+#ifndef NW_ROWE64
+#define NW_ROWE64 32
+#endif
+template <typename T, int N2> constexpr int kRowE = N2 >= 8192 ? (sizeof(T) == 4 ? 32 : NW_ROWE64) : 16;
+// complex table rows (wavelet_bin loads) spill at fp64 E = 32: E = 16 there
+template <typename T, int N2> constexpr int kRowETab = sizeof(T) == 8 ? 16 : kRowE<T, N2>;
 // elements per thread in cols_kernel: 32 complex fp32 or 16 complex fp64 (64 VGPRs either way)
 template <typename T> constexpr int kColE = sizeof(T) == 4 ? 32 : 16;
 template <typename T> constexpr int kMaxN2 = sizeof(T) == 4 ? 16384 : 8192;
@@ -573,7 +578,7 @@ hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, 
                 case NW_MORSE: return launch_row_pass<T, NN, EE, NW_MORSE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
                 case NW_MORLET: return launch_row_pass<T, NN, EE, NW_MORLET>(d, f0, nf, sp.n1, Xt, B, km, s);   \
                 case NW_SHANNON: return launch_row_pass<T, NN, EE, NW_SHANNON>(d, f0, nf, sp.n1, Xt, B, km, s); \
-                case NW_TABLE: return launch_row_pass<T, NN, EE, NW_TABLE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
+                case NW_TABLE: return launch_row_pass<T, NN, kRowETab<T, NN>, NW_TABLE>(d, f0, nf, sp.n1, Xt, B, km, s); \
                 default: return hipErrorNotSupported;                                                        \
             }                                                                                                \
         }                                                                                                    \
