@@ -47,7 +47,11 @@ constexpr int kRowTileG = 8;      // row groups per XCD tile
 #ifndef NW_COL_THREADS
 #define NW_COL_THREADS 1024   // C = 32 columns at N1 = 1024: 256-B runs; measured C5 cols 1.039 -> 0.978 ms vs 512
 #endif
-constexpr int kColThreads = NW_COL_THREADS;  // cols_kernel workgroup size (C * N1 / E)
+#ifndef NW_COL_THREADS64
+#define NW_COL_THREADS64 1024
+#endif
+// cols_kernel workgroup size (C * N1 / E)
+template <typename T> constexpr int kColThreads = sizeof(T) == 4 ? NW_COL_THREADS : NW_COL_THREADS64;
 constexpr size_t kBBudget = size_t(2) << 30;   // bytes of B per launch pair (scales chunked to fit)
 
 // N2 (on-chip rows) and its elements per thread E: the nw_fused sizes (fp64: E = 16, N2 <= 8192)
@@ -268,9 +272,9 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_
 template <typename T, int N1> struct Cols {
     static constexpr int E = kColE<T>;
     static constexpr int U = N1 / E;                 // threads per column
-    static constexpr int C = kColThreads / U;        // columns per workgroup
+    static constexpr int C = kColThreads<T> / U;     // columns per workgroup
     using G = Geometry<N1, E>;
-    static_assert(N1 >= 32 && C >= (sizeof(T) == 4 ? 16 : 8), "cols geometry");
+    static_assert(N1 >= 32 && C >= (sizeof(T) == 4 ? 16 : 4), "cols geometry");
 };
 
 template <typename T, int N1, int P, int COMP>
@@ -371,7 +375,7 @@ constexpr int kSplitLo = 4096;
 constexpr int kSplitEntries = 2 * kSplitLo;   // n <= 2^24: m >> 12 < 4096
 
 template <typename T, int N1, int N2, int OUT>
-__global__ __launch_bounds__(kColThreads, sizeof(T) == 8 ? 2 : 4) void cols_kernel(
+__global__ __launch_bounds__(kColThreads<T>, sizeof(T) == 8 ? 2 : 4) void cols_kernel(
     int f0, int nf, const C2<T>* __restrict__ B, void* __restrict__ out, const C2<T>* __restrict__ tw1,
     const C2<T>* __restrict__ tsplit) {
     using CL = Cols<T, N1>;
@@ -485,11 +489,11 @@ hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, 
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     if (out_kind == NW_OUT_CWT)
-        cols_kernel<T, N1, N2, NW_OUT_CWT><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out, tw1, tsplit);
+        cols_kernel<T, N1, N2, NW_OUT_CWT><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     else if (out_kind == NW_OUT_POWER)
-        cols_kernel<T, N1, N2, NW_OUT_POWER><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out, tw1, tsplit);
+        cols_kernel<T, N1, N2, NW_OUT_POWER><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     else
-        cols_kernel<T, N1, N2, NW_OUT_ABS><<<(unsigned)blocks, kColThreads, lds, s>>>(f0, nf, B, out, tw1, tsplit);
+        cols_kernel<T, N1, N2, NW_OUT_ABS><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     return hipGetLastError();
 }
 
