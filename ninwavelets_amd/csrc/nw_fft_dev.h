@@ -55,6 +55,16 @@ __device__ __forceinline__ C2<float> hi(C2<f2> p) { return {p.re.y, p.im.y}; }
 template <typename T> __device__ __forceinline__ C2<T> cmul(C2<T> a, C2<T> b) {
     return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
+// a pair of complex numbers (two signals) times one complex number (a shared twiddle):
+// the scalar operand is splat across both halves of every packed op
+__device__ __forceinline__ C2<f2> cmul(C2<f2> a, C2<float> b) {
+    return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
+}
+
+// scalar type of a lane value: C2<f2> carries two signals' values of one float element
+template <typename T> struct ScalarOf { using type = T; };
+template <> struct ScalarOf<f2> { using type = float; };
+template <typename T> using Sc = typename ScalarOf<T>::type;
 
 // --- memory ops addressed as wave-uniform base (SGPR pair) + 32-bit per-lane byte
 // offset: `global_load/store ... v_off, s[base:base+1]` (saddr form), i.e. one VGPR
@@ -180,12 +190,12 @@ __device__ __forceinline__ void twiddle_bases(C2<T>* p, int m, const C2<T>* __re
         }
     }
 }
-template <typename T, int R>
-__device__ __forceinline__ void twiddle_apply(C2<T>* v, const C2<T>* p) {
+template <typename T, int R, typename P>
+__device__ __forceinline__ void twiddle_apply(C2<T>* v, const C2<P>* p) {
     constexpr int LR = ilog2<R>();
 #pragma unroll
     for (int r = 1; r < R; ++r) {
-        C2<T> w = p[__builtin_ctz(r)];
+        C2<P> w = p[__builtin_ctz(r)];
 #pragma unroll
         for (int k = __builtin_ctz(r) + 1; k < LR; ++k)
             if (r & (1 << k)) w = cmul(w, p[k]);
@@ -365,18 +375,19 @@ template <int N, int E, int P, int OSZ = 8> struct PassInfo {
 #endif
 template <typename T, int N, int E> struct Tab1 {
     using I = PassInfo<N, E, 1>;
+    using S = Sc<T>;                                // entries in the scalar type (shared by a pair)
     static constexpr int NS = I::NS, R = I::R;
     static constexpr int COUNT = Geometry<N, E>::npass() >= 2 ? NS * (R - 1) : 0;
-    static constexpr bool ON = NW_TAB1 && COUNT > 0 && COUNT * (int)sizeof(C2<T>) <= 8192;
-    static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<T>) : 0;
+    static constexpr bool ON = NW_TAB1 && COUNT > 0 && COUNT * (int)sizeof(C2<S>) <= 8192;
+    static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<S>) : 0;
     static_assert((lds_elems<N, E>() * sizeof(T)) % 16 == 0, "table alignment");
-    __device__ static __forceinline__ const C2<T>* table(const T* lds) {
-        return reinterpret_cast<const C2<T>*>(lds + lds_elems<N, E>());
+    __device__ static __forceinline__ const C2<S>* table(const T* lds) {
+        return reinterpret_cast<const C2<S>*>(lds + lds_elems<N, E>());
     }
     // w_N^e entries from the exact table tw (tw[i] = exp(+2 pi i / N))
-    __device__ static __forceinline__ void fill(T* lds, const C2<T>* __restrict__ tw, int t) {
+    __device__ static __forceinline__ void fill(T* lds, const C2<S>* __restrict__ tw, int t) {
         if constexpr (ON) {
-            C2<T>* tab = reinterpret_cast<C2<T>*>(lds + lds_elems<N, E>());
+            C2<S>* tab = reinterpret_cast<C2<S>*>(lds + lds_elems<N, E>());
             for (int i = t; i < COUNT; i += Geometry<N, E>::T) {
                 const int jj = i % NS, r = i / NS + 1;
                 tab[i] = tw[(jj * r * (N / (NS * R))) % N];
@@ -594,20 +605,26 @@ template <typename T, int N, int E> constexpr int kLdsBytes =
 // before this signal's stores are issued: loads, stores and LDS-DMA retire in one
 // in-order vmcnt queue, so the next pass 0 waits for that DMA only.  The last pass
 // stores its outputs straight to HBM.
+//
+// T = f2 (signal pairs): every element carries two signals' values; twiddles and the Tab1
+// table stay scalar (shared), and the last pass stores the low halves to ocur and the high
+// halves to ocur2 (nullptr: an odd last signal, its high half is not stored).
 template <typename T, int N, int E, int OUT, int P, bool XD>
-__device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>* __restrict__ tw, C2<T>* x,
+__device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
-                                            Stamps* st) {
-    constexpr int OSZ = (int)sizeof(typename OutT<OUT, T>::type);
+                                            Stamps* st, void* ocur2 = nullptr) {
+    using S = Sc<T>;
+    constexpr bool PAIRSIG = !std::is_same<T, S>::value;
+    constexpr int OSZ = (int)sizeof(typename OutT<OUT, S>::type);
     using I = PassInfo<N, E, P, OSZ>;
     if constexpr (P < Geometry<N, E>::npass()) {
         constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
         constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;
-        C2<T> pb[Q][LR > 0 ? LR : 1];
+        C2<S> pb[Q][LR > 0 ? LR : 1];
 #ifndef NW_ABL_NOTWIDDLE
         if constexpr (!TABLED) {
 #pragma unroll
-            for (int q = 0; q < Q; ++q) twiddle_bases<T, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
+            for (int q = 0; q < Q; ++q) twiddle_bases<S, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
         }
 #endif
 #ifndef NW_ABL_NOEXCH
@@ -639,17 +656,17 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
         for (int q = 0; q < Q; ++q) {
 #ifndef NW_ABL_NOTWIDDLE
             if constexpr (TABLED) {
-                const C2<T>* tab = Tab1<T, N, E>::table(lds) + I::bfly(t, q) % I::NS;
+                const C2<S>* tab = Tab1<T, N, E>::table(lds) + I::bfly(t, q) % I::NS;
 #pragma unroll
                 for (int r = 1; r < R; ++r) {
                     v[q * R + r] = cmul(v[q * R + r], tab[(r - 1) * I::NS]);
                     if (r % 8 == 7) __builtin_amdgcn_sched_barrier(0);   // <= 8 twiddles in flight
                 }
-            } else if constexpr (!(NW_PK && sizeof(T) == 4 && Q % 2 == 0)) {
+            } else if constexpr (!(NW_PK && std::is_same<T, float>::value && Q % 2 == 0)) {
                 twiddle_apply<T, R>(v + q * R, pb[q]);
             }
 #endif
-            if constexpr (NW_PK && sizeof(T) == 4 && Q % 2 == 0) {
+            if constexpr (NW_PK && std::is_same<T, float>::value && Q % 2 == 0) {
                 // butterflies q, q+1 as one packed pair: identical DIF networks, per-butterfly
                 // twiddles packed side by side
                 if (q % 2 == 0) {
@@ -681,9 +698,20 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<T>
         NW_STAMP(st, 2 * P);                   // pass P arithmetic
         if constexpr (I::LAST) {
             __builtin_amdgcn_sched_barrier(0);
-            LastStores<T, N, E, OUT>::all(v, ocur, t);
+            if constexpr (PAIRSIG) {
+                C2<S> a[E], b[E];
+#pragma unroll
+                for (int i = 0; i < E; ++i) {
+                    a[i] = C2<S>{v[i].re.x, v[i].im.x};
+                    b[i] = C2<S>{v[i].re.y, v[i].im.y};
+                }
+                LastStores<S, N, E, OUT>::all(a, ocur, t);
+                if (ocur2) LastStores<S, N, E, OUT>::all(b, ocur2, t);
+            } else {
+                LastStores<T, N, E, OUT>::all(v, ocur, t);
+            }
         } else {
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st);
+            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2);
         }
     }
 }

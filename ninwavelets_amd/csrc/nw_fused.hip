@@ -225,6 +225,74 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
 #endif
 }
 
+// Signal pairs (fp32, E = 16, analytic real W rows): the block's signals are transformed
+// two at a time, each lane value a C2<f2> holding signal s in the low and s+1 in the high
+// half, so every butterfly, twiddle multiply and LDS access of the FFT serves two signals
+// (v_pk_add/mul/fma_f32; 8-B image slots; twiddles and the pass-1 table shared).  Pass 0
+// reads both X rows and the block's W registers; the last pass stores each half to its
+// own row (an odd last signal transforms a duplicate whose high half is not stored).
+#ifndef NW_PAIR
+#define NW_PAIR 1
+#endif
+#ifndef NW_WPS_PAIR
+#define NW_WPS_PAIR 4
+#endif
+template <int N, int E, int OUT>
+__global__ __launch_bounds__(N / E, NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc d, const cplx<float>* __restrict__ X,
+                                                                  const void* __restrict__ wtab, void* __restrict__ out,
+                                                                  const C2<float>* __restrict__ tw, int64_t nsig,
+                                                                  int group, int nsg_pad, const int* __restrict__ wnz) {
+    using G = Geometry<N, E>;
+    static_assert(E <= 16, "pair mode holds 2 x E complex values per lane");
+    extern __shared__ __align__(16) unsigned char smem[];
+    f2* lds = reinterpret_cast<f2*>(smem);
+    const int t = threadIdx.x;
+    // XCD-aware block -> (scale, signal group): as nw_fused_kernel
+    const int b = blockIdx.x;
+    const int xcd = b & 7;
+    const int local = b >> 3;
+    const int pos = local % (kTileF * kTileG);
+    const int round = local / (kTileF * kTileG);
+    const int nfr = (d.nfreq + kTileF - 1) / kTileF;
+    const int fi = (round % nfr) * kTileF + pos % kTileF;
+    const int sg = ((round / nfr) * kTileG + pos / kTileF) * 8 + xcd;
+    if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
+    const int64_t s_begin = (int64_t)sg * group;
+    const int64_t s_end = min(nsig, s_begin + group);
+
+    const float* wrow = reinterpret_cast<const float*>(wtab) + (int64_t)fi * N;
+    const uint32_t wo = (uint32_t)t * (uint32_t)sizeof(float);
+    float w[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(float)));
+    Tab1<f2, N, E>::fill(lds, tw, t);
+    const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<float>) : sizeof(float));
+    const int nz = NW_PRUNE ? wnz[fi] : E;
+    for (int64_t s = s_begin; s < s_end; s += 2) {
+        const bool two = s + 1 < s_end;
+        const int64_t s2 = two ? s + 1 : s;
+        C2<f2> v[E];
+        auto pass0 = [&]<int NZ>() {
+            C2<float> xa[E], xb[E];
+            load_x<float, N, E, NZ>(xa, reinterpret_cast<const C2<float>*>(X + s * d.nh), t);
+            load_x<float, N, E, NZ>(xb, reinterpret_cast<const C2<float>*>(X + s2 * d.nh), t);
+#pragma unroll
+            for (int r = 0; r < E; ++r)
+                v[r] = r < NZ ? C2<f2>{f2{w[r] * xa[r].re, w[r] * xb[r].re}, f2{w[r] * xa[r].im, w[r] * xb[r].im}}
+                              : C2<f2>{f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
+            idft_br<f2, E, NZ>(v);
+        };
+        if (NW_PRUNE_MIN <= 1 && nz <= 1) pass0.template operator()<1>();
+        else if (NW_PRUNE_MIN <= 2 && nz <= 2) pass0.template operator()<2>();
+        else if (nz <= 4) pass0.template operator()<4>();
+        else if (nz <= 8) pass0.template operator()<8>();
+        else pass0.template operator()<E>();
+        void* o1 = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;
+        void* o2 = two ? (void*)((char*)out + (s2 * d.nfreq + fi) * (int64_t)N * out_esz) : nullptr;
+        passes_from<f2, N, E, OUT, 1, false>(v, lds, t, tw, nullptr, nullptr, o1, nullptr, o2);
+    }
+}
+
 // W[f, k] for the fused engine: the reference's cached row, pad_to'd to n, 1/n folded
 // in (real rows for analytic kinds, complex for tables).  Built once per plan+wavelet.
 template <typename T, bool REALW>
@@ -326,6 +394,9 @@ size_t wtab_row_bytes(int64_t n, int nfreq, size_t esz, bool realw) {
     return (b + 15) / 16 * 16;
 }
 
+template <typename T, int E, bool REALW>
+constexpr bool kPairMode = NW_PAIR && std::is_same<T, float>::value && E <= 16 && REALW;
+
 template <typename T, int N, int E, bool REALW>
 hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
                     hipStream_t s) {
@@ -343,6 +414,18 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     const C2<T>* twc_ = reinterpret_cast<const C2<T>*>(tw);
     const int* wnz = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
                                                   wtab_row_bytes(N, d.nfreq, sizeof(T), REALW));
+    if constexpr (kPairMode<T, E, REALW>) {
+        const size_t lp = (size_t)kLdsBytes<f2, N, E>;
+        const C2<float>* twf = reinterpret_cast<const C2<float>*>(tw);
+        const cplx<float>* Xf = reinterpret_cast<const cplx<float>*>(X);
+        if (out_kind == NW_OUT_CWT)
+            nw_fused_pair_kernel<N, E, NW_OUT_CWT><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz);
+        else if (out_kind == NW_OUT_POWER)
+            nw_fused_pair_kernel<N, E, NW_OUT_POWER><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz);
+        else
+            nw_fused_pair_kernel<N, E, NW_OUT_ABS><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz);
+        return hipGetLastError();
+    }
     if (out_kind == NW_OUT_CWT)
         nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad, wnz);
     else if (out_kind == NW_OUT_POWER)
@@ -354,6 +437,18 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
 
 template <typename T, int N, int E, bool REALW>
 hipError_t prepare_one() {
+    if constexpr (kPairMode<T, E, REALW>) {
+        const int lp = kLdsBytes<f2, N, E>;
+        hipError_t e = hipFuncSetAttribute((const void*)nw_fused_pair_kernel<N, E, NW_OUT_CWT>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, lp);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)nw_fused_pair_kernel<N, E, NW_OUT_POWER>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lp);
+        if (e == hipSuccess)
+            e = hipFuncSetAttribute((const void*)nw_fused_pair_kernel<N, E, NW_OUT_ABS>,
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, lp);
+        if (e != hipSuccess) return e;
+    }
     const int lds = kLdsBytes<T, N, E>;
     hipError_t e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
