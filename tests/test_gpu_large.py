@@ -155,6 +155,10 @@ def test_large_fp64_outputs_batch_table_and_rocfft_agreement():
         assert rel_err(a[s], np.abs(ref)) <= 1e-12
     r = nw.Morse(1000, engine='rocfft').cwt_batch(x, freqs)
     assert rel_err(c, r) <= 1e-12
+    pm = w.cwt_batch(x, freqs, out='power_mean')            # epoch reduction over the batch
+    assert rel_err(pm, np.mean(np.abs(c) ** 2, axis=0)) <= 1e-13
+    itc = w.cwt_batch(x, freqs, out='itc')
+    assert np.max(np.abs(itc - np.abs(np.mean(c / np.abs(c), axis=0)))) <= 1e-12
     wi = nw.Morse(1000, interpolate=True)
     assert rel_err(wi.cwt(x[0], freqs), O.cwt('morse', x[0], freqs, interpolate=True)) <= 1e-12
     assert large_ran(wi)
