@@ -63,7 +63,10 @@ template <typename T, int N2> constexpr int kRowE = N2 >= 8192 ? (sizeof(T) == 4
 template <typename T, int N2> constexpr int kRowETab = sizeof(T) == 8 ? 16 : kRowE<T, N2>;
 // elements per thread in cols_kernel: 32 complex fp32 or 16 complex fp64 (64 VGPRs either way)
 template <typename T> constexpr int kColE = sizeof(T) == 4 ? 32 : 16;
-template <typename T> constexpr int kMaxN2 = sizeof(T) == 4 ? 16384 : 8192;
+#ifndef NW_MAXN2_64
+#define NW_MAXN2_64 16384   // measured at C5 fp64: 8192 (N1 = 2048, 8-column blocks, 128-B runs) 150.0 ms/step, 16384 (N1 = 1024, 16 columns, 256-B runs) 129.9
+#endif
+template <typename T> constexpr int kMaxN2 = sizeof(T) == 4 ? 16384 : NW_MAXN2_64;
 
 // ---- X (R2C half spectrum) -> Xt[k1][k2], mirrored + masked (spectrum_bin)
 template <typename T>
@@ -608,8 +611,13 @@ hipError_t cols_t(const WDesc& d, int out_kind, int f0, int nf, const void* supp
         NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(32, 16384)
         NW_COLS(64, 16384) NW_COLS(128, 16384) NW_COLS(256, 16384) NW_COLS(512, 16384) NW_COLS(1024, 16384)
     } else {
+#if NW_MAXN2_64 == 8192
         NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(64, 8192)
         NW_COLS(128, 8192) NW_COLS(256, 8192) NW_COLS(512, 8192) NW_COLS(1024, 8192) NW_COLS(2048, 8192)
+#else
+        NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(32, 16384)
+        NW_COLS(64, 16384) NW_COLS(128, 16384) NW_COLS(256, 16384) NW_COLS(512, 16384) NW_COLS(1024, 16384)
+#endif
     }
     return hipErrorNotSupported;
 #undef NW_COLS
