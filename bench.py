@@ -177,8 +177,9 @@ def main():
         out_kind = args.output
     if args.samples:
         n = args.samples
-    if args.dtype:
+    if args.dtype and args.dtype != dtype:
         dtype = args.dtype
+        text += f' [compute dtype overridden: {dtype}, outputs in {dtype} / its complex type]'
     S = epochs * chans                       # signals on this rank
     F = len(freqs)
     C = min(args.chunk or DEFAULT_CHUNK.get(args.config, 256), S)
