@@ -443,8 +443,10 @@ typedef __attribute__((address_space(1))) void gbl_void_t;
 
 // LDS-DMA of X[0 .. N/2) (the R2C half spectrum without its Nyquist bin) into LDS at dst:
 // 16 B per lane per instruction, wave w filling its own 1 KiB slices of each round.
+// nround < CH / TT copies only the first nround rounds (2*TT bins each): the bins a pruned
+// pass 0 reads (wave-uniform count)
 template <typename T, int N, int TT>
-__device__ __forceinline__ void dma_x(const C2<T>* xs, void* dst, int t) {
+__device__ __forceinline__ void dma_x(const C2<T>* xs, void* dst, int t, int nround = 1 << 30) {
     constexpr int CH = (N / 2) * (int)sizeof(C2<T>) / 16;   // 16-byte chunks
     static_assert(CH % TT == 0, "whole DMA rounds");
     // wave-uniform LDS destination base in an SGPR (M0 takes it directly; a VGPR copy
@@ -453,6 +455,7 @@ __device__ __forceinline__ void dma_x(const C2<T>* xs, void* dst, int t) {
     const uint32_t lane_off = (uint32_t)t * 16u;
 #pragma unroll
     for (int i = 0; i < CH / TT; ++i) {
+        if (i >= nround) break;
         // uniform chunk base + opaque 32-bit lane offset: the saddr form, no 64-bit VGPR pairs
         const char* chunk = reinterpret_cast<const char*>(xs) + (size_t)i * TT * 16;
         asm volatile("" : "+s"(chunk));           // computed here, in SGPRs (not hoisted)
@@ -612,7 +615,7 @@ template <typename T, int N, int E> constexpr int kLdsBytes =
 template <typename T, int N, int E, int OUT, int P, bool XD>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
-                                            Stamps* st, void* ocur2 = nullptr) {
+                                            Stamps* st, void* ocur2 = nullptr, int dma_rounds = 1 << 30) {
     using S = Sc<T>;
     constexpr bool PAIRSIG = !std::is_same<T, S>::value;
     constexpr int OSZ = (int)sizeof(typename OutT<OUT, S>::type);
@@ -647,7 +650,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
         if constexpr (I::LAST && XD) {
             if (xs_next) {                     // the image is idle once every wave has read it
                 lds_barrier();
-                dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t);
+                dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t, dma_rounds);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -711,7 +714,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                 LastStores<T, N, E, OUT>::all(v, ocur, t);
             }
         } else {
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2);
+            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds);
         }
     }
 }

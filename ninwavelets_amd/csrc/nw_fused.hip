@@ -69,6 +69,9 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
 // Occupancy target: 4 waves per SIMD (<= 128 VGPRs).  The half image is <= 74 KiB
 // (fp32), so two 512-thread blocks share a CU at n = 16384 (more at smaller n) and
 // one block's barriers, memory waits and store bursts overlap another's arithmetic.
+#ifndef NW_DMA_PRUNE
+#define NW_DMA_PRUNE 1   // LDS-DMA of X limited to the pruned pass 0's bins
+#endif
 #ifndef NW_GROUP
 #define NW_GROUP 8   // measured: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (with NW_TILEG 4)
 #endif
@@ -155,13 +158,20 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     C2<T> nyq{T(0), T(0)};
     if constexpr (XD || XB) {
         nyq = reinterpret_cast<const C2<T>*>(X + s_begin * d.nh)[N / 2];
+        const int nz0 = NW_PRUNE ? wnz[fi] : E;
+        const int nzv0 = nz0 < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz0;
         dma_x<T, N, G::T>(reinterpret_cast<const C2<T>*>(X + s_begin * d.nh),
-                          XD ? (void*)lds : (void*)XBuf<T, N, E>::at_lds(lds), t);
+                          XD ? (void*)lds : (void*)XBuf<T, N, E>::at_lds(lds), t,
+                          (XD && NW_DMA_PRUNE && nzv0 <= E / 2) ? (nzv0 + 1) / 2 : 1 << 30);
     }
     // W row support (device-built with the table): elements r >= nz of pass 0 multiply an
     // exactly-zero W for every thread of the block (k = t + r*T beyond the row's last
     // nonzero bin), so they are neither read nor multiplied and the DIF stages skip them
     const int nz = NW_PRUNE ? wnz[fi] : E;
+    // LDS-DMA only the X bins the pruned pass 0 reads: variant NZ (>= 4) reads bins < NZ*T,
+    // i.e. NZ/2 rounds of 2*T bins, when it reads no mirrored bin (NZ <= E/2)
+    const int nzv = nz < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz;
+    const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? (nzv + 1) / 2 : 1 << 30;
     for (int64_t s = s_begin; s < s_end; ++s) {
         const C2<T>* xl = nullptr;
         if constexpr (XD || XB) {
@@ -213,7 +223,7 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
         void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
-        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, ocur, st);
+        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds);
     }
     // the last signal's outputs
     NW_STAMP(st, kStampsStore);
