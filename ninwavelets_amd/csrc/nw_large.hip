@@ -1,4 +1,5 @@
-// nw_large.hip — the fused CWT engine for long power-of-two signals (fp32, n = 2^15 .. 2^24).
+// nw_large.hip — the fused CWT engine for long power-of-two signals (fp32 and fp64,
+// n = 2^15 .. 2^24).
 //
 // One output row y_f = ifft_n(W_f * X) (reference base.py:378-407: scipy ifft, 1/n folded
 // into W) is longer than one workgroup's LDS holds, so it is computed as a four-step
@@ -16,9 +17,13 @@
 //                bin), a length-N2 inverse FFT on chip (the nw_fused pass machinery), the
 //                complex row stored to B[f][k1][0 .. N2)
 //   cols_kernel  per (scale f, C consecutive n2): v[k1] = B[f][k1][n2] * w_n^(n2 k1), C
-//                length-N1 inverse FFTs side by side (C * N1 = 32768 points per 1024-thread
-//                workgroup, C * 8 B contiguous per k1 read), epilogue y / |y| / |y|^2 stored
-//                to out[f][n2 + N2 n1] (C * 8 B = 256-B contiguous runs at N1 = 1024)
+//                length-N1 inverse FFTs side by side (C * N1 = 32768 fp32 / 16384 fp64 points
+//                per 1024-thread workgroup, C * 2e B contiguous per k1 read), epilogue y / |y|
+//                / |y|^2 stored to out[f][n2 + N2 n1] (256-B contiguous runs at N1 = 1024)
+//
+// fp64: E = 32 rows (16 for table rows), 16 elements per thread in the column pass, the
+// column twiddles from two exact split tables and a per-thread recurrence, Morse rows in
+// the log domain (RowW<double>).
 //
 // Measured at C5 (1 x 2^24 x 512, tools/ablate.sh): the column pass is bound by its
 // mixed read + write HBM stream (4.4 TB/s combined; without its stores it reads at
