@@ -153,6 +153,9 @@ def main():
     ap.add_argument('--samples', type=int, default=None, help='override the signal length (diagnostics)')
     ap.add_argument('--dtype', default=None, choices=['float32', 'float64'],
                     help='override the compute dtype (diagnostics)')
+    ap.add_argument('--wavelet', default=None, choices=['morse', 'morlet', 'shannon'],
+                    help="override the config's wavelet (C5 is 'Shannon + Morse': --config c5 "
+                         "--wavelet shannon is its Shannon line)")
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 
@@ -177,6 +180,12 @@ def main():
         out_kind = args.output
     if args.samples:
         n = args.samples
+    if args.wavelet and args.wavelet != kind:
+        text = text.replace(kind.capitalize(), args.wavelet.capitalize(), 1)
+        kind = args.wavelet
+        if kind == 'shannon':
+            text += (' [Shannon ignores the freq (wavelets.py:256-262): its one distinct row is '
+                     'computed once per signal and copied to every scale]')
     if args.dtype and args.dtype != dtype:
         dtype = args.dtype
         text += f' [compute dtype overridden: {dtype}, outputs in {dtype} / its complex type]'
@@ -191,7 +200,7 @@ def main():
     plan = nw.Plan(n, F, dtype, device=local, max_batch=C,
                    engine=None if args.engine == 'auto' else args.engine, timing=True)
     grid = L.trans_grid(n / 1000., 1000., False)
-    params = {'morse': [17.5, 3.0], 'morlet': [7.0, 0.0]}[kind]
+    params = {'morse': [17.5, 3.0], 'morlet': [7.0, 0.0], 'shannon': []}[kind]
     plan.set_wavelet(kind, params, freqs, grid)
     esz = 8 if f64 else 4
     x_ptr, x_row = x.data_ptr(), n * esz
@@ -238,7 +247,21 @@ def main():
         if not fused:
             out_e = 2 * esz                    # K1 always writes the complex product
         extra = {}
-        if two_pass:
+        uniq = st['unique_rows']
+        if uniq < F and st['launches_expand'] > 0:
+            # repeated rows (Shannon): the engine computed `uniq` rows per signal and
+            # k_expand_rows wrote every output row, reading each computed row once -- the
+            # expand kernel moves the dominant bytes
+            comp_ms = (st['ms_fused'] + st['ms_rows'] + st['ms_multiply'] + st['ms_inverse'] +
+                       st['ms_epilogue']) / args.steps
+            extra['computed_rows'] = {'unique_rows': uniq, 'engine_ms_per_step': round(comp_ms, 3),
+                                      'engine_launches': launches}
+            ex_l = st['launches_expand']
+            ms = st['ms_expand'] / ex_l
+            out_e = (2 if out_kind == 'cwt' else 1) * esz
+            per_launch = float(S) * F * n * args.steps / ex_l * out_e * (1 + uniq / F)
+            kname = 'k_expand_rows'
+        elif two_pass:
             # column pass (the kernel that writes the output): reads B once (2e B/pt, complex
             # in the compute dtype) and writes each output point once; the row pass writes B
             # once and reads the transposed spectrum Xt once per launch (from L2 across the
@@ -256,15 +279,17 @@ def main():
                 'achieved': round(rows_bytes / (rows_ms * 1e-3) / 1e9, 1), 'peak': PEAK_HBM_GBPS,
                 'unit': 'GB/s', 'frac': round(rows_bytes / (rows_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
                 'avg_launch_ms': round(rows_ms, 4), 'algorithmic_bytes_per_launch': rows_bytes}
+        else:
+            per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
+            kname = 'nw_fused' if fused else 'k1_multiply'
+        if two_pass or kname == 'k_expand_rows':
             # end to end against the path's minimum traffic (X read once, every output once)
-            min_bytes = float(S) * ((n // 2 + 1) * 2 * esz + F * n * out_e)
+            oe = (2 if out_kind == 'cwt' else 1) * esz
+            min_bytes = float(S) * ((n // 2 + 1) * 2 * esz + F * n * oe)
             extra['end_to_end_min_traffic'] = {
                 'bytes_per_step': min_bytes,
                 'achieved': round(min_bytes / (el / args.steps) / 1e9, 1), 'unit': 'GB/s',
                 'frac': round(min_bytes / (el / args.steps) / 1e9 / PEAK_HBM_GBPS, 4)}
-        else:
-            per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
-            kname = 'nw_fused' if fused else 'k1_multiply'
         achieved = per_launch / (ms * 1e-3) / 1e9
         roof = {'kernel': kname, 'bound': 'hbm',
                 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
@@ -272,7 +297,8 @@ def main():
                 'traffic': pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind),
                 'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
         stage_ms = {k: round(st[k] / args.steps, 3) for k in
-                    ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_rows', 'ms_copy')}
+                    ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_rows', 'ms_expand',
+                     'ms_copy')}
         cpu = cpu_pool = None
         if world == 1 and not args.no_cpu_baseline:
             log('[bench] cpu baseline ...')

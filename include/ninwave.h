@@ -60,6 +60,10 @@ extern "C" {
 #define NW_ENGINE_FUSED  0x20u /* force: rocFFT fwd -> fused multiply+LDS inverse FFT+epilogue
                                   (n > 16384: the two-pass form, nw_large.hip)                  */
 #define NW_TIMING        0x100u/* record HIP events around every stage (nw_plan_stats)            */
+#define NW_NO_DEDUP      0x200u/* compute every scale row even when wavelet rows repeat (by
+                                  default rows with identical W -- Shannon ignores f
+                                  (wavelets.py:256-262), repeated freqs -- are computed once
+                                  and copied: bit-identical output, nw_stats.unique_rows)      */
 
 /* execute outputs */
 #define NW_OUT_CWT   0   /* complex (S, F, N)   base.py:378-407 */
@@ -105,6 +109,9 @@ typedef struct nw_stats {
                                pass 2, the column FFTs + epilogue; the spectrum transpose is
                                timed in ms_copy) */
     int64_t launches_rows;
+    double  ms_expand;      /* repeated rows: copies of the computed unique rows */
+    int64_t launches_expand;
+    int64_t unique_rows;    /* scale rows actually computed (nfreq unless rows repeat) */
 } nw_stats;
 
 typedef struct nw_plan nw_plan;

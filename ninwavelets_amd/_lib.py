@@ -32,6 +32,7 @@ NW_INTERPOLATE = 0x1
 NW_ENGINE_ROCFFT = 0x10
 NW_ENGINE_FUSED = 0x20
 NW_TIMING = 0x100
+NW_NO_DEDUP = 0x200
 NW_OUT_CWT, NW_OUT_ABS, NW_OUT_POWER = 0, 1, 2
 NW_OUT_POWER_MEAN, NW_OUT_ITC, NW_OUT_POWER_SUM, NW_OUT_PHASE_SUM = 3, 4, 5, 6
 NW_MEM_HOST, NW_MEM_DEVICE = 0, 1
@@ -49,7 +50,8 @@ class nw_stats(ctypes.Structure):
                 ('ms_fused', ctypes.c_double), ('ms_copy', ctypes.c_double),
                 ('launches_multiply', ctypes.c_int64), ('launches_fused', ctypes.c_int64),
                 ('engine', ctypes.c_int64), ('ms_rows', ctypes.c_double),
-                ('launches_rows', ctypes.c_int64)]
+                ('launches_rows', ctypes.c_int64), ('ms_expand', ctypes.c_double),
+                ('launches_expand', ctypes.c_int64), ('unique_rows', ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

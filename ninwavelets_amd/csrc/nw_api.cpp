@@ -17,6 +17,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "nw_internal.h"
@@ -65,7 +66,7 @@ struct DeviceGuard {
     }
 };
 
-enum Stage { ST_FWD = 0, ST_MUL, ST_INV, ST_EPI, ST_FUSED, ST_COPY, ST_ROWS, ST_N };
+enum Stage { ST_FWD = 0, ST_MUL, ST_INV, ST_EPI, ST_FUSED, ST_COPY, ST_ROWS, ST_EXPAND, ST_N };
 
 struct Pending {
     int stage;
@@ -93,6 +94,19 @@ struct nw_plan {
     void* d_table = nullptr;
     int64_t* d_row_len = nullptr;
     std::vector<int64_t> row_len_host;   // tables: true length of each row
+
+    // repeated rows: when at most half the F rows of W are distinct (Shannon ignores f,
+    // wavelets.py:256-262; repeated freqs), the engines run on the U distinct rows
+    // (udesc, compacted per-freq arrays) into d_uout and k_expand_rows copies each
+    // computed row to every scale that repeats it (d_rep_offs / d_rep_order: the scales
+    // grouped by distinct row).  NW_NO_DEDUP turns it off.
+    bool dedup = false;
+    int nuniq = 0;
+    nw::WDesc udesc{};
+    void* d_ubuf = nullptr;          // udesc's freq / peak / xstep32 / row_len (+ table rows)
+    int32_t* d_rep = nullptr;        // offs[U + 1] then order[F]
+    void* d_uout = nullptr;
+    size_t d_uout_bytes = 0;
 
     // buffers
     void* d_x = nullptr;
@@ -158,6 +172,7 @@ void count_launch(nw_plan* p, int stage) {
         case ST_MUL: p->stats.launches_multiply++; break;
         case ST_FUSED: p->stats.launches_fused++; break;
         case ST_ROWS: p->stats.launches_rows++; break;
+        case ST_EXPAND: p->stats.launches_expand++; break;
         default: break;
     }
 }
@@ -189,6 +204,7 @@ int resolve_timing(nw_plan* p) {
             case ST_EPI: p->stats.ms_epilogue += ms; break;
             case ST_FUSED: p->stats.ms_fused += ms; break;
             case ST_ROWS: p->stats.ms_rows += ms; break;
+            case ST_EXPAND: p->stats.ms_expand += ms; break;
             default: p->stats.ms_copy += ms; break;
         }
         p->event_pool.push_back(pe.a);
@@ -257,7 +273,7 @@ int run_fft_rows(nw_plan* p, bool inverse, int64_t rows, char* in, char* out, si
     return NW_OK;
 }
 
-int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
+int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     const bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
     // rocFFT may use its input as scratch: transform from the plan's own copy.
     if (xs_dev != p->d_x)
@@ -341,6 +357,43 @@ int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind
     }
     return staged(p, ST_EPI, [&] {
         NW_HIP(nw::launch_epilogue(p->dtype, out_kind, Y, dst, c * p->nfreq * p->n, p->stream));
+        return NW_OK;
+    });
+}
+
+// The engines see the plan as if it had only the U distinct rows (desc, nfreq); the
+// execute-time geometry nw_execute set on desc is carried over.
+struct UniqueRows {
+    nw_plan* p;
+    nw::WDesc saved;
+    explicit UniqueRows(nw_plan* pl) : p(pl), saved(pl->desc) {
+        nw::WDesc u = p->udesc;
+        u.n = saved.n;
+        u.nh = saved.nh;
+        u.scale = saved.scale;
+        u.off = saved.off;
+        u.xlim = saved.xlim;
+        p->desc = u;
+        p->nfreq = p->nuniq;
+    }
+    ~UniqueRows() {
+        p->desc = saved;
+        p->nfreq = saved.nfreq;
+    }
+};
+
+// One device chunk: (c, F, n) outputs of kind out_kind into dst (device).
+int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
+    if (!p->dedup) return run_chunk_rows(p, xs_dev, c, dst, out_kind, dst_is_final);
+    const size_t row = (size_t)p->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
+    NW_TRY(ensure(&p->d_uout, &p->d_uout_bytes, (size_t)c * p->nuniq * row));
+    {
+        UniqueRows u(p);   // d_uout is scratch of the CWT's row size: K1 may write it
+        NW_TRY(run_chunk_rows(p, xs_dev, c, p->d_uout, out_kind, true));
+    }
+    return staged(p, ST_EXPAND, [&] {
+        NW_HIP(nw::launch_expand_rows(p->d_uout, dst, c, p->nuniq, p->nfreq, row, p->d_rep, p->d_rep + p->nuniq + 1,
+                                      p->stream));
         return NW_OK;
     });
 }
@@ -461,7 +514,8 @@ void free_plan(nw_plan* p) {
     for (auto& kv : p->inv) rocfft_plan_destroy(kv.second);
     if (p->info) rocfft_execution_info_destroy(p->info);
     void* bufs[] = {p->work,   p->d_x,    p->d_X,        p->d_Y,     p->d_out,      p->d_wtab,
-                    p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len, p->d_acc, p->d_scratch};
+                    p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len, p->d_acc, p->d_scratch,
+                    p->d_ubuf, p->d_rep,  p->d_uout};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& pe : p->pending) {
@@ -696,6 +750,122 @@ static int build_normal_table(nw_plan* p, int kind, const double* params, int np
     return rc;
 }
 
+// Distinct rows of W (see nw_plan::dedup).  A row is a function of (kind, params, grid)
+// and, except for Shannon, of its freq (tables: of its contents), so equal freqs (equal
+// table rows) give bit-identical outputs.  rep[f] = first scale with the same row.
+static int setup_unique_rows(nw_plan* p, int kind, const double* freqs, const std::vector<double>& peak,
+                             const std::vector<float>& xstep, const void* host_table) {
+    const int F = p->nfreq;
+    p->dedup = false;
+    p->nuniq = F;
+    p->stats.unique_rows = F;
+    if (p->d_ubuf) NW_HIP(hipFree(p->d_ubuf));
+    if (p->d_rep) NW_HIP(hipFree(p->d_rep));
+    p->d_ubuf = nullptr;
+    p->d_rep = nullptr;
+    std::vector<int> rep(F);
+    std::vector<int> uniq;   // first scale of every distinct row, in order
+    if (kind == NW_SHANNON) {
+        std::fill(rep.begin(), rep.end(), 0);
+        uniq.push_back(0);
+    } else if (kind == NW_TABLE && host_table) {
+        // user rows: equal length and equal contents (hash, then compare)
+        const int64_t L = p->desc.len_full;
+        const double* t = (const double*)host_table;
+        std::unordered_map<uint64_t, std::vector<int>> seen;
+        for (int f = 0; f < F; ++f) {
+            const int64_t len = p->row_len_host.empty() ? L : p->row_len_host[f];
+            const unsigned char* b = (const unsigned char*)(t + (size_t)f * L * 2);
+            uint64_t h = 1469598103934665603ull ^ (uint64_t)len;
+            for (size_t i = 0; i < (size_t)len * 16; ++i) h = (h ^ b[i]) * 1099511628211ull;
+            int found = -1;
+            for (int g : seen[h]) {
+                const int64_t lg = p->row_len_host.empty() ? L : p->row_len_host[g];
+                if (lg == len && std::memcmp(b, t + (size_t)g * L * 2, (size_t)len * 16) == 0) {
+                    found = g;
+                    break;
+                }
+            }
+            if (found < 0) {
+                seen[h].push_back(f);
+                uniq.push_back(f);
+                rep[f] = f;
+            } else {
+                rep[f] = found;
+            }
+        }
+    } else {
+        // analytic kinds and Normal tables: a row is a function of its freq (bitwise)
+        std::unordered_map<uint64_t, int> first;
+        for (int f = 0; f < F; ++f) {
+            uint64_t key;
+            std::memcpy(&key, &freqs[f], sizeof(key));
+            auto it = first.find(key);
+            if (it == first.end()) {
+                first.emplace(key, f);
+                uniq.push_back(f);
+                rep[f] = f;
+            } else {
+                rep[f] = it->second;
+            }
+        }
+    }
+    const int U = (int)uniq.size();
+    if ((p->flags & NW_NO_DEDUP) || 2 * U > F) return NW_OK;
+    // scales grouped by distinct row: offs[u] .. offs[u + 1] index order[]
+    std::vector<int> uidx(F, -1), counts(U, 0);
+    for (int u = 0; u < U; ++u) uidx[uniq[u]] = u;
+    for (int f = 0; f < F; ++f) counts[uidx[rep[f]]]++;
+    std::vector<int32_t> host(U + 1 + F);
+    host[0] = 0;
+    for (int u = 0; u < U; ++u) host[u + 1] = host[u] + counts[u];
+    std::vector<int> fill(host.begin(), host.begin() + U);
+    for (int f = 0; f < F; ++f) host[U + 1 + fill[uidx[rep[f]]]++] = f;
+    // compacted per-freq arrays of the distinct rows
+    const nw::WDesc& d = p->desc;
+    const bool table = d.kind == NW_TABLE;
+    const size_t trow = table ? (size_t)d.len_full * 2 * p->esz : 0;
+    const size_t o_peak = (size_t)U * 8, o_x = o_peak + (size_t)U * 8, o_rl = (o_x + (size_t)U * 4 + 15) / 16 * 16,
+                 o_tab = (o_rl + (size_t)U * 8 + 255) / 256 * 256, bytes = o_tab + (size_t)U * trow;
+    std::vector<double> uf(U), up(U);
+    std::vector<float> ux(U);
+    std::vector<int64_t> url(U, d.len_full);
+    for (int u = 0; u < U; ++u) {
+        uf[u] = freqs[uniq[u]];
+        up[u] = peak[uniq[u]];
+        ux[u] = xstep[uniq[u]];
+        if (table && !p->row_len_host.empty()) url[u] = p->row_len_host[uniq[u]];
+    }
+    char* b = nullptr;
+    NW_HIP(hipMalloc((void**)&b, bytes));
+    p->d_ubuf = b;
+    NW_HIP(hipMemcpy(b, uf.data(), U * 8, hipMemcpyHostToDevice));
+    NW_HIP(hipMemcpy(b + o_peak, up.data(), U * 8, hipMemcpyHostToDevice));
+    NW_HIP(hipMemcpy(b + o_x, ux.data(), U * 4, hipMemcpyHostToDevice));
+    nw::WDesc u = d;
+    u.nfreq = U;
+    u.freq = (const double*)b;
+    u.peak = (const double*)(b + o_peak);
+    u.xstep32 = (const float*)(b + o_x);
+    if (table) {
+        if (d.row_len) {
+            NW_HIP(hipMemcpy(b + o_rl, url.data(), U * 8, hipMemcpyHostToDevice));
+            u.row_len = (const int64_t*)(b + o_rl);
+        }
+        for (int k = 0; k < U && trow > 0; ++k)
+            NW_HIP(hipMemcpy(b + o_tab + (size_t)k * trow, (const char*)d.table + (size_t)uniq[k] * trow, trow,
+                             hipMemcpyDeviceToDevice));
+        u.table = b + o_tab;
+    }
+    NW_HIP(hipMalloc((void**)&p->d_rep, host.size() * sizeof(int32_t)));
+    NW_HIP(hipMemcpy(p->d_rep, host.data(), host.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    p->udesc = u;
+    p->nuniq = U;
+    p->dedup = true;
+    p->stats.unique_rows = U;
+    return NW_OK;
+}
+
 int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams, const double* freqs,
                         const nw_grid* grid, const void* table, const int64_t* row_len) {
     if (!p || !freqs || !grid) return fail(NW_E_INVALID, "nw_plan_set_wavelet: null argument");
@@ -794,7 +964,7 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
     p->desc = d;
     p->has_wavelet = true;
     p->wtab_valid = false;
-    return NW_OK;
+    return setup_unique_rows(p, kind, freqs, peak, xstep, normal ? nullptr : table);
 }
 
 int nw_plan_wavelet_shape(nw_plan* p, int64_t* len_full, int64_t* row_len) {
@@ -1138,9 +1308,10 @@ int nw_plan_reset_stats(nw_plan* p) {
     if (!p) return fail(NW_E_INVALID, "nw_plan_reset_stats: null plan");
     DeviceGuard guard(p->device);
     NW_TRY(resolve_timing(p));
-    const int64_t engine = p->stats.engine;
+    const int64_t engine = p->stats.engine, uniq = p->stats.unique_rows;
     p->stats = nw_stats{};
     p->stats.engine = engine;
+    p->stats.unique_rows = uniq;
     return NW_OK;
 }
 

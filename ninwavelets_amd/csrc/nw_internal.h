@@ -124,6 +124,9 @@ __device__ __forceinline__ cplx<T> spectrum_bin(const cplx<T>* __restrict__ Xs, 
 hipError_t launch_multiply(const WDesc& d, int dtype, const void* X, void* Y, int64_t nsig, hipStream_t s);
 hipError_t launch_epilogue(int dtype, int out_kind, const void* Y, void* out, int64_t count, hipStream_t s);
 hipError_t launch_rows(const WDesc& d, int dtype, void* rows, hipStream_t s);
+// repeated rows: dst (nsig, nf, row) from src (nsig, nu, row), scales grouped by distinct row
+hipError_t launch_expand_rows(const void* src, void* dst, int64_t nsig, int nu, int nf, size_t row_bytes,
+                              const int32_t* offs, const int32_t* order, hipStream_t s);
 // epoch reductions: source kinds of launch_accumulate
 enum { ACC_POWER_REAL = 0, ACC_POWER_Y = 1, ACC_PHASE_Y = 2 };
 hipError_t launch_accumulate(int dtype, int src_kind, const void* src, double* acc, int64_t fn, int64_t c,

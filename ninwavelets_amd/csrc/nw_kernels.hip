@@ -6,11 +6,14 @@
 //   baseline               Baseline correction                   (base.py:18-68)
 //   normal_time / finish   MexicanHat / Haar rows on the device  (base.py:249-256)
 //   wavelet_*              time-domain wavelets, make_wavelet(s)  (base.py:346-376)
+//   expand_rows            copies of repeated scale rows (Shannon ignores f)
 //
 // K1 is HBM-write bound (8 or 16 B per output point, X re-read from L2): each
 // block evaluates W for one scale f and a 256*V-bin tile ONCE into registers,
 // then sweeps a group of signals, so the transcendental cost of psi is
 // amortised over the group.  Stores are 16 B per lane (float4 / double2).
+#include <type_traits>
+
 #include "nw_internal.h"
 
 namespace nw {
@@ -456,6 +459,48 @@ hipError_t launch_baseline(int dtype, const void* x, int64_t count, int64_t b0, 
         k_bl_final<1><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
         if (count > 0) k_bl_apply<double><<<ab, 256, 0, s>>>((const double*)x, (double*)out, count, op, stats);
     }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Repeated rows (nw_plan::dedup): dst[s][f][:] = src[s][u][:] for every scale f whose
+// wavelet row is the u-th distinct one (order[offs[u] .. offs[u + 1])).  Each block
+// reads one tile of a computed row once and streams it to all of its copies, so the
+// HBM traffic is the output write plus 1/(F/U) of it read: write-bound.
+// ---------------------------------------------------------------------------
+template <typename V>
+__global__ __launch_bounds__(256) void k_expand_rows(const V* __restrict__ src, V* __restrict__ dst, int64_t rowv,
+                                                     int64_t tiles, int64_t nblk, int nu, int nf,
+                                                     const int32_t* __restrict__ offs,
+                                                     const int32_t* __restrict__ order) {
+    for (int64_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const int64_t su = b / tiles;               // s * nu + u
+        const int64_t k = (b - su * tiles) * 256 + threadIdx.x;
+        if (k >= rowv) continue;
+        const int u = (int)(su % nu);
+        const V v = src[su * rowv + k];
+        V* base = dst + (su / nu) * nf * rowv + k;
+        const int i1 = offs[u + 1];
+        for (int i = offs[u]; i < i1; ++i) __builtin_nontemporal_store(v, base + (int64_t)order[i] * rowv);
+    }
+}
+
+hipError_t launch_expand_rows(const void* src, void* dst, int64_t nsig, int nu, int nf, size_t row_bytes,
+                              const int32_t* offs, const int32_t* order, hipStream_t s) {
+    using V4 = unsigned int __attribute__((ext_vector_type(4)));
+    using V2 = unsigned int __attribute__((ext_vector_type(2)));
+    auto go = [&](auto* tag, size_t vb) {
+        using V = std::remove_pointer_t<decltype(tag)>;
+        const int64_t rowv = (int64_t)(row_bytes / vb);
+        const int64_t tiles = (rowv + 255) / 256;
+        const int64_t nblk = nsig * nu * tiles;
+        if (nblk == 0) return;
+        const int64_t grid = std::min<int64_t>(nblk, int64_t(1) << 20);
+        k_expand_rows<V><<<(unsigned)grid, 256, 0, s>>>((const V*)src, (V*)dst, rowv, tiles, nblk, nu, nf, offs, order);
+    };
+    if (row_bytes % 16 == 0) go((V4*)nullptr, 16);
+    else if (row_bytes % 8 == 0) go((V2*)nullptr, 8);
+    else go((unsigned int*)nullptr, 4);
     return hipGetLastError();
 }
 

@@ -51,7 +51,8 @@ class Plan:
     """One nw_plan: signals of length ``n``, ``nfreq`` scales, compute ``dtype``."""
 
     def __init__(self, n: int, nfreq: int, dtype='float32', device: int = 0, max_batch: int = 1,
-                 interpolate: bool = False, engine: str | None = None, timing: bool = False):
+                 interpolate: bool = False, engine: str | None = None, timing: bool = False,
+                 dedup: bool = True):
         self.n, self.nfreq, self.device, self.max_batch = int(n), int(nfreq), int(device), int(max_batch)
         self.dtype = np_dtype(dtype)
         self.interpolate = bool(interpolate)
@@ -64,6 +65,8 @@ class Plan:
             raise ValueError(f'engine must be rocfft, fused or auto, got {engine!r}')
         if timing:
             flags |= L.NW_TIMING
+        if not dedup:            # compute every scale row even when wavelet rows repeat
+            flags |= L.NW_NO_DEDUP
         self._h = ctypes.c_void_p()
         L.check(L.lib().nw_plan_create(ctypes.byref(self._h), self.device, self.n, self.max_batch,
                                        self.nfreq, L.NW_F32 if self.dtype == np.float32 else L.NW_F64,
