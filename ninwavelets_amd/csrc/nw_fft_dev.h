@@ -327,6 +327,25 @@ template <int COMP, typename T> __device__ __forceinline__ T& comp(C2<T>& c) {
 template <typename T, int N, int E, int P, int COMP>
 __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
     using G = Geometry<N, E>;
+#ifdef NW_ABL_ADDTID
+    // diagnostic only (wrong results): the same bytes written as lane-contiguous
+    // ds_write_addtid_b32 (no address VGPR, 128 B/clk/CU) -- what cheaper exchange writes buy
+    {
+        constexpr int W = sizeof(T) / 4;
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+            T x = comp<COMP>(v[i]);
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(&x);
+#pragma unroll
+            for (int k = 0; k < W; ++k)
+                asm volatile("s_mov_b32 m0, 0\n\tds_write_addtid_b32 %0 offset:%1" ::"v"(d[k]), "i"(((i * W + k) % 64) * 256)
+                             : "memory");   // m0 is reserved: the compiler re-sets it before its own uses
+        }
+        (void)lds;
+        (void)t;
+        return;
+    }
+#endif
     if constexpr (P == 0) {
         Pair<T>* dst = reinterpret_cast<Pair<T>*>(lds + lds_idx<E>(t * E));
 #pragma unroll
