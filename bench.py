@@ -156,6 +156,10 @@ def main():
     ap.add_argument('--wavelet', default=None, choices=['morse', 'morlet', 'shannon'],
                     help="override the config's wavelet (C5 is 'Shannon + Morse': --config c5 "
                          "--wavelet shannon is its Shannon line)")
+    ap.add_argument('--shard', default='signals', choices=['signals', 'scales'],
+                    help='what the ranks split: signals (weak scaling, every rank its own epochs) '
+                         'or the scale list of the same signals (strong scaling; the C5 split for '
+                         'one long signal, SURVEY §8e)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     args = ap.parse_args()
 
@@ -191,9 +195,15 @@ def main():
         text += f' [compute dtype overridden: {dtype}, outputs in {dtype} / its complex type]'
     S = epochs * chans                       # signals on this rank
     F = len(freqs)
+    F_all, by_scales = F, args.shard == 'scales' and world > 1
+    if by_scales:                            # this rank: a contiguous slice of the scales
+        from ninwavelets_amd.dist import shard
+        f0, f1 = shard(F, rank, world)
+        freqs = freqs[f0:f1]
+        F = f1 - f0
     C = min(args.chunk or DEFAULT_CHUNK.get(args.config, 256), S)
     f64 = dtype == 'float64'
-    x = synth_device(torch, S, n, seed=1000 + rank, device=dev, dtype=torch.float64 if f64 else torch.float32)
+    x = synth_device(torch, S, n, seed=1000 + (0 if by_scales else rank), device=dev, dtype=torch.float64 if f64 else torch.float32)
     odt = {('cwt', False): torch.complex64, ('cwt', True): torch.complex128}.get(
         (out_kind, f64), torch.float64 if f64 else torch.float32)
     bufs = [torch.empty((C, F, n), dtype=odt, device=dev) for _ in range(1 if C >= S else 2)]
@@ -234,7 +244,7 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
     st = plan.stats()
-    points = float(S) * F * n * args.steps * world
+    points = float(S) * F_all * n * args.steps * (1 if by_scales else world)
     value = points / el
 
     if rank == 0:
@@ -312,10 +322,13 @@ def main():
             'metric': 'CWT throughput (epochs*chans*samples*freqs)/s',
             'value': value, 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64' if f64 else 'f32', 'data': 'synthetic',
-            'config': {'workload': text, 'wavelet': kind, 'epochs': epochs * world, 'chans': chans,
-                       'samples': n, 'freqs': F, 'output': out_kind, 'engine': st['engine'],
-                       'chunk_signals': C, 'parallelism': f'dp{world} (signals sharded, no collective)'},
+            'scaling': 'strong' if by_scales else 'weak', 'vs_baseline': None, 'dtype': 'f64' if f64 else 'f32', 'data': 'synthetic',
+            'config': {'workload': text, 'wavelet': kind, 'epochs': epochs * (1 if by_scales else world),
+                       'chans': chans, 'samples': n, 'freqs': F_all, 'output': out_kind, 'engine': st['engine'],
+                       'chunk_signals': C,
+                       'parallelism': (f'scales{world} (each rank a contiguous slice of the scales, '
+                                       f'no collective)' if by_scales else
+                                       f'dp{world} (signals sharded, no collective)')},
             'roofline': roof, **extra, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool, 'stage_ms_per_step': stage_ms,
         }
         print(json.dumps(line), flush=True)

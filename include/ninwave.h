@@ -174,6 +174,16 @@ int nw_execute(nw_plan* plan, const void* x, int64_t nsig, void* out, int out_ki
 int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t nsig,
                      void* out, int out_kind);
 
+/* Shard the SCALES instead (one long signal, e.g. C5, cannot shard by
+ * signal): plan i (its own device, same n / dtype / flags) holds the i-th contiguous
+ * slice of the scale list, nfreq_i scales, sum nfreq_i = F.  Every device transforms all
+ * nsig host signals for its scales (its own forward FFT: ~0.2 ms at 2^24, cheaper than a
+ * broadcast) and writes its rows of out (nsig, F, n) -- or (F, n) for the reduction
+ * kinds -- in place; no exchange.  Meant for nsig below the device count (the host
+ * output is written one signal at a time). */
+int nw_execute_multi_scales(nw_plan* const* plans, int nplans, const void* x, int64_t nsig,
+                            void* out, int out_kind);
+
 /* Baseline correction (base.py:18-68: class Baseline; baseline_of at 18-20) of a real
  * array x[count] (dtype NW_F32 / NW_F64).  The reference slices AXIS 0: for an array
  * whose rows hold row_len elements the baseline is rows [row0, row1) (already

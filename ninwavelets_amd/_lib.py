@@ -75,6 +75,7 @@ SIGNATURES = [
     ('nw_plan_wavelet_rows', ctypes.c_int, [_P, _P]),
     ('nw_execute', ctypes.c_int, [_P, _P, _I64, _P, ctypes.c_int, ctypes.c_int]),
     ('nw_execute_multi', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),
+    ('nw_execute_multi_scales', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),
     ('nw_baseline', ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _I64, _I64, _I64, _I64, ctypes.c_int, _P,
                                    ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     ('nw_make_wavelets', ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int,

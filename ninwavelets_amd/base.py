@@ -274,9 +274,12 @@ class WaveletBase:
         self._rows = None
 
     # ------------------------------------------------------------------ execution
-    def _plan(self, n: int, nsig: int, device: int) -> Plan:
+    def _plan(self, n: int, nsig: int, device: int, scales: tuple[int, int] | None = None) -> Plan:
+        """The cached plan for (n, batch, device) -- of the scale slice [f0, f1) when
+        ``scales`` is given (scale-sharded multi-device calls)."""
         c = self._cache
-        nf = len(c.freqs)
+        f0, f1 = scales if scales is not None else (0, len(c.freqs))
+        nf = f1 - f0
         esz = self.dtype.itemsize
         per_sig = nf * n * esz * 5 + n * esz * 3
         cap = max(1, CHUNK_BYTES // per_sig)
@@ -284,21 +287,32 @@ class WaveletBase:
         while batch < min(nsig, cap):
             batch *= 2
         batch = min(batch, cap)
-        key = (n, nf, self.dtype.str, bool(self.interpolate), device, batch, self.engine)
+        key = (n, nf, self.dtype.str, bool(self.interpolate), device, batch, self.engine, f0)
         plan = self._plans.get(key)
         if plan is None:
             plan = Plan(n, nf, self.dtype, device, batch, self.interpolate, self.engine)
             self._plans[key] = plan
         if plan.wavelet_token != c.version:
-            plan.set_wavelet(c.kind, c.params, c.freqs, c.grid, c.table, token=c.version,
-                             row_len=c.row_len)
+            sl = slice(f0, f1)
+            plan.set_wavelet(c.kind, c.params, c.freqs[sl], c.grid,
+                             None if c.table is None else c.table[sl], token=c.version,
+                             row_len=None if c.row_len is None else c.row_len[sl])
         return plan
 
     def _run(self, x: np.ndarray, out_kind: str) -> np.ndarray:
-        """x: (..., n) signals -> (..., F, n) on the device(s)."""
+        """x: (..., n) signals -> (..., F, n) on the device(s).  Several devices shard the
+        signals, or -- with fewer signals than devices (one long signal) -- the scales."""
         n = x.shape[-1]
         nsig = int(np.prod(x.shape[:-1])) if x.ndim > 1 else 1
         devs = self.devices or [self.device]
+        nf = len(self._cache.freqs)
+        if len(devs) > 1 and nsig < len(devs) and nf >= len(devs):
+            from .dist import shard
+            plans = [self._plan(n, nsig, d, shard(nf, i, len(devs))) for i, d in enumerate(devs)]
+            out = execute_multi(plans, x.reshape(nsig, n), out_kind, shard='scales')
+            if out_kind in REDUCTIONS:
+                return out
+            return out.reshape(x.shape[:-1] + out.shape[-2:])
         if len(devs) > 1 and nsig > 1:
             per = -(-nsig // len(devs))
             plans = [self._plan(n, per, d) for d in devs]

@@ -1123,6 +1123,52 @@ int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t n
     return NW_OK;
 }
 
+int nw_execute_multi_scales(nw_plan* const* plans, int nplans, const void* x, int64_t nsig, void* out,
+                            int out_kind) {
+    if (!plans || nplans < 1 || !plans[0]) return fail(NW_E_INVALID, "nw_execute_multi_scales: no plans");
+    const nw_plan* p0 = plans[0];
+    for (int i = 1; i < nplans; ++i)
+        if (!plans[i] || plans[i]->n != p0->n || plans[i]->dtype != p0->dtype ||
+            (plans[i]->flags & NW_INTERPOLATE) != (p0->flags & NW_INTERPOLATE))
+            return fail(NW_E_INVALID, "nw_execute_multi_scales: plans must share n, dtype and interpolate");
+    if (out_kind < NW_OUT_CWT || out_kind > NW_OUT_PHASE_SUM)
+        return fail(NW_E_INVALID, "nw_execute_multi_scales: bad out_kind");
+    if (nsig < 0) return fail(NW_E_INVALID, "nw_execute_multi_scales: nsig < 0");
+    if (nsig > 0 && (!x || !out)) return fail(NW_E_INVALID, "nw_execute_multi_scales: null argument");
+    int64_t F = 0;
+    std::vector<int64_t> f0(nplans);
+    for (int i = 0; i < nplans; ++i) {
+        f0[i] = F;
+        F += plans[i]->nfreq;
+    }
+    // bytes of one output element: reductions keep their own types (include/ninwave.h)
+    size_t oe = (out_kind == NW_OUT_CWT ? 2 : 1) * p0->esz;
+    if (out_kind == NW_OUT_POWER_SUM) oe = sizeof(double);
+    if (out_kind == NW_OUT_PHASE_SUM) oe = 2 * sizeof(double);
+    const size_t x_row = (size_t)p0->n * p0->esz, o_scale = (size_t)p0->n * oe;
+    std::vector<int> rc(nplans, NW_OK);
+    std::vector<std::string> err(nplans);
+    std::vector<std::thread> th;
+    for (int i = 0; i < nplans; ++i) {
+        th.emplace_back([&, i] {
+            nw_plan* p = plans[i];
+            if (is_reduction(out_kind) || nsig <= 1) {   // the rows are contiguous in out
+                rc[i] = nw_execute(p, x, nsig, (char*)out + f0[i] * o_scale, out_kind, NW_MEM_HOST);
+            } else {
+                for (int64_t s = 0; s < nsig && rc[i] == NW_OK; ++s)
+                    rc[i] = nw_execute(p, (const char*)x + s * x_row, 1,
+                                       (char*)out + ((size_t)s * F + f0[i]) * o_scale, out_kind, NW_MEM_HOST);
+            }
+            if (rc[i] != NW_OK) err[i] = g_last_error;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int i = 0; i < nplans; ++i)
+        if (rc[i] != NW_OK)
+            return fail(rc[i], "device " + std::to_string(plans[i]->device) + ": " + err[i]);
+    return NW_OK;
+}
+
 int nw_baseline(int device, int dtype, const void* x, int64_t count, int64_t row_len, int64_t row0, int64_t row1,
                 int op, void* out, int mem, double* stats) {
     if (dtype != NW_F32 && dtype != NW_F64) return fail(NW_E_INVALID, "nw_baseline: dtype must be NW_F32 or NW_F64");

@@ -7,6 +7,11 @@ exchange is the epoch reduction of EpochsWavelet.power / itc (mneutils.py:42-71)
 each rank sums its block in fp64 on its device (``power_sum`` / ``phase_sum``),
 one all_reduce adds the partial sums, and every rank finalises the mean -- F x n
 values per collective, independent of the number of epochs.
+
+One long signal (C5: 1 x 2^24) cannot shard by signal: there the ranks split the SCALE
+list instead (``shard(nfreq, rank, world)``, each rank computing every signal for its
+contiguous slice, its own forward FFT, no exchange), and ``gather_scales`` is the
+optional all_gather of the slices when one process needs the whole (..., F, n) result.
 """
 from __future__ import annotations
 
@@ -78,3 +83,31 @@ def epochs_reduce(wavelet, waves: np.ndarray, freqs, kind: str, group=None) -> n
     if dist.get_backend(group) == 'nccl':
         dev = torch.device('cuda', torch.cuda.current_device())
     return reduce_partials(part, kind, nsig, wavelet.dtype, group, dev)
+
+
+def gather_scales(local: np.ndarray, nfreq: int, group=None, device=None) -> np.ndarray:
+    """All ranks' scale slices -> the full (..., nfreq, n) array on every rank.  ``local``
+    is this rank's (..., f1 - f0, n) result for ``shard(nfreq, rank, world)``; slices are
+    padded to ceil(nfreq / world) rows for the fixed-size all_gather and trimmed after.
+    ``device``: where the collective runs (a CUDA device for RCCL; None = CPU for gloo)."""
+    import torch
+    import torch.distributed as dist
+    world = dist.get_world_size(group)
+    per = -(-nfreq // world)
+    loc = np.ascontiguousarray(local)
+    pad = np.zeros(loc.shape[:-2] + (per, loc.shape[-1]), dtype=loc.dtype)
+    pad[..., :loc.shape[-2], :] = loc
+    t = torch.from_numpy(pad)
+    if t.is_complex():
+        t = torch.view_as_real(t)
+    if device is not None:
+        t = t.to(device)
+    parts = [torch.empty_like(t) for _ in range(world)]
+    dist.all_gather(parts, t, group=group)
+    rows = []
+    for r, part in enumerate(parts):
+        part = part.cpu()
+        a = torch.view_as_complex(part).numpy() if np.iscomplexobj(loc) else part.numpy()
+        f0, f1 = shard(nfreq, r, world)
+        rows.append(a[..., :f1 - f0, :])
+    return np.concatenate(rows, axis=-2)

@@ -194,17 +194,25 @@ class Plan:
             pass
 
 
-def execute_multi(plans, x: np.ndarray, out_kind: str = 'cwt') -> np.ndarray:
-    """Shard host signals over several single-device plans (one host thread each)."""
+def execute_multi(plans, x: np.ndarray, out_kind: str = 'cwt', shard: str = 'signals') -> np.ndarray:
+    """Several single-device plans, one host thread each.
+    shard='signals': identical plans, contiguous blocks of the host signals per device
+    (nw_execute_multi).  shard='scales': plan i holds the i-th contiguous slice of the
+    scale list and transforms every signal for it (nw_execute_multi_scales) -- the split
+    for one long signal (C5)."""
+    if shard not in ('signals', 'scales'):
+        raise ValueError(f"shard must be 'signals' or 'scales', got {shard!r}")
     p0 = plans[0]
     x = np.ascontiguousarray(x, dtype=p0.dtype)
     lead = x.shape[:-1]
     nsig = int(np.prod(lead)) if lead else 1
-    shape = (p0.nfreq, p0.n) if out_kind in REDUCTIONS else lead + (p0.nfreq, p0.n)
+    nf = sum(p.nfreq for p in plans) if shard == 'scales' else p0.nfreq
+    shape = (nf, p0.n) if out_kind in REDUCTIONS else lead + (nf, p0.n)
     out = np.empty(shape, dtype=out_dtype(p0.dtype, out_kind))
     arr = (ctypes.c_void_p * len(plans))(*[p.handle.value for p in plans])
-    L.check(L.lib().nw_execute_multi(arr, len(plans), x.ctypes.data_as(ctypes.c_void_p), nsig,
-                                     out.ctypes.data_as(ctypes.c_void_p), OUT_KINDS[out_kind]))
+    fn = L.lib().nw_execute_multi_scales if shard == 'scales' else L.lib().nw_execute_multi
+    L.check(fn(arr, len(plans), x.ctypes.data_as(ctypes.c_void_p), nsig,
+               out.ctypes.data_as(ctypes.c_void_p), OUT_KINDS[out_kind]))
     return out
 
 

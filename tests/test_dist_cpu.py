@@ -59,6 +59,35 @@ def _worker(rank, world, port, E, out_dir):
         dist.destroy_process_group()
 
 
+def _scale_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        x = epochs(1, n=1024)[0]
+        f0, f1 = D.shard(len(FREQS), rank, world)
+        # this rank's slice of the scales (the oracle stands in for the rank's device)
+        local = np.stack([O.cwt('morse', x, [f, f])[0] for f in FREQS[f0:f1]]) if f1 > f0 \
+            else np.zeros((0, x.size), dtype=np.complex128)
+        full = D.gather_scales(local, len(FREQS))
+        np.save(os.path.join(out_dir, f'scales{rank}.npy'), full)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_scale_sharded_ranks_gather_the_full_cwt(tmp_path, world):
+    """One signal, scales split over ranks: every rank computes its
+    contiguous slice and gather_scales rebuilds the (F, n) result on every rank."""
+    import torch.multiprocessing as mp
+    mp.spawn(_scale_worker, args=(world, free_port(), str(tmp_path)), nprocs=world, join=True)
+    x = epochs(1, n=1024)[0]
+    ref = O.cwt('morse', x, FREQS)
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f'scales{r}.npy'), ref)
+
+
 def test_shard_blocks_cover_every_signal_once():
     for nsig in [0, 1, 2, 7, 64, 1000, 262144]:
         for world in [1, 2, 3, 8]:
