@@ -66,13 +66,19 @@ def synth_device(torch, S, n, seed, device, sfreq=1000., dtype=None):
 
 def pmc_traffic(kernel, config, chunk, engine, dtype='float32', out=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    same bench command (tools/gpu_round.sh -> profiles/pmc_<config>_<engine>.json), or None
+    same bench command (tools/gpu_round.sh -> profiles/pmc_<config>_<engine>.json, or
+    profiles/pmc_<config>_<kernel>.json for a second kernel of one config), or None
     when the summary was taken on another kernel, chunk, dtype or output kind."""
-    path = os.path.join(ROOT, 'profiles', f'pmc_{config}_{engine}.json')
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
+    d = None
+    for name in (f'pmc_{config}_{engine}.json', f'pmc_{config}_{kernel}.json'):
+        try:
+            with open(os.path.join(ROOT, 'profiles', name)) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get('kernel') == kernel:
+            break
+    if d is None:
         return None
     c = d.get('config', {})
     if d.get('kernel') != kernel or c.get('chunk') != chunk or c.get('dtype', 'float32') != dtype:
@@ -291,7 +297,8 @@ def main():
                 'avg_launch_ms': round(rows_ms, 4), 'algorithmic_bytes_per_launch': rows_bytes}
         else:
             per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
-            kname = 'nw_fused' if fused else 'k1_multiply'
+            chirp = fused and (n < 1024 or n & (n - 1))      # nw_chirp.hip: two on-chip FFTs per row
+            kname = ('nw_chirp_kernel' if chirp else 'nw_fused') if fused else 'k1_multiply'
         if two_pass or kname == 'k_expand_rows':
             # end to end against the path's minimum traffic (X read once, every output once)
             oe = (2 if out_kind == 'cwt' else 1) * esz

@@ -58,8 +58,13 @@ extern "C" {
 #define NW_INTERPOLATE   0x1u  /* zero the upper half of fft(x) (interpolate_alias, base.py:400-401) */
 #define NW_ENGINE_ROCFFT 0x10u /* force: rocFFT fwd -> K1 multiply -> rocFFT inv -> K2 epilogue   */
 #define NW_ENGINE_FUSED  0x20u /* force: rocFFT fwd -> fused multiply+LDS inverse FFT+epilogue
-                                  (n > 16384: the two-pass form, nw_large.hip)                  */
+                                  (n > 16384: the two-pass form, nw_large.hip; n not a power
+                                  of two >= 1024 with 2n-1 <= 16384 fp32 / 8192 fp64: the
+                                  chirp-z form, nw_chirp.hip)                                  */
 #define NW_TIMING        0x100u/* record HIP events around every stage (nw_plan_stats)            */
+#define NW_NO_CHIRP      0x400u/* auto engine: keep the rocFFT engine for lengths the chirp-z fused
+                                  form would take (non-power-of-two n, 2n-1 <= 16384 fp32 /
+                                  8192 fp64, and n < 1024)                                     */
 #define NW_NO_DEDUP      0x200u/* compute every scale row even when wavelet rows repeat (by
                                   default rows with identical W -- Shannon ignores f
                                   (wavelets.py:256-262), repeated freqs -- are computed once

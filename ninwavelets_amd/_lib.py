@@ -33,6 +33,7 @@ NW_ENGINE_ROCFFT = 0x10
 NW_ENGINE_FUSED = 0x20
 NW_TIMING = 0x100
 NW_NO_DEDUP = 0x200
+NW_NO_CHIRP = 0x400
 NW_OUT_CWT, NW_OUT_ABS, NW_OUT_POWER = 0, 1, 2
 NW_OUT_POWER_MEAN, NW_OUT_ITC, NW_OUT_POWER_SUM, NW_OUT_PHASE_SUM = 3, 4, 5, 6
 NW_MEM_HOST, NW_MEM_DEVICE = 0, 1

@@ -121,6 +121,7 @@ struct nw_plan {
     size_t d_wtab_bytes = 0;
     bool wtab_valid = false;
     bool large = false;              // fused engine, two-pass form (nw_large.hip)
+    bool chirp = false;              // fused engine, chirp-z form (nw_chirp.hip): other n
     void* d_scratch = nullptr;       // two-pass form: Xt + B
     size_t d_scratch_bytes = 0;
 
@@ -318,6 +319,18 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
             }
         }
         return NW_OK;
+    }
+    if (!rocfft_engine && p->chirp) {
+        // chirp-z form (any other n up to 8192 fp32 / 4096 fp64): two on-chip FFTs per row
+        if (!p->wtab_valid) {
+            NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes, nw::chirp_wtable_bytes(p->n, p->nfreq, p->dtype, p->desc.kind)));
+            NW_HIP(nw::build_chirp_wtable(p->desc, p->dtype, p->d_wtab, p->stream));
+            p->wtab_valid = true;
+        }
+        return staged(p, ST_FUSED, [&] {
+            NW_HIP(nw::launch_chirp(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->stream));
+            return NW_OK;
+        });
     }
     if (!rocfft_engine) {
         if (!p->wtab_valid) {
@@ -584,7 +597,7 @@ int nw_trans_grid(double real_length, double sfreq, int interpolate, nw_grid* g)
 }
 
 int nw_fused_supported(int64_t n, int dtype) {
-    return nw::fused_supported(n, dtype) || nw::large_supported(n, dtype) ? 1 : 0;
+    return nw::fused_supported(n, dtype) || nw::large_supported(n, dtype) || nw::chirp_supported(n, dtype) ? 1 : 0;
 }
 
 int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int32_t nfreq, int dtype,
@@ -612,7 +625,8 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     p->flags = flags;
     p->esz = dtype == NW_F32 ? 4 : 8;
     const bool large_ok = !nw::fused_supported(n, dtype) && nw::large_supported(n, dtype);
-    const bool fused_ok = nw::fused_supported(n, dtype) || large_ok;
+    const bool chirp_ok = nw::chirp_supported(n, dtype) && !(flags & NW_NO_CHIRP);
+    const bool fused_ok = nw::fused_supported(n, dtype) || large_ok || chirp_ok;
     if (flags & NW_ENGINE_FUSED) {
         if (!fused_ok) {
             free_plan(p);
@@ -625,6 +639,7 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
         p->engine = fused_ok ? NW_ENGINE_FUSED : NW_ENGINE_ROCFFT;
     }
     p->large = p->engine == NW_ENGINE_FUSED && large_ok;
+    p->chirp = p->engine == NW_ENGINE_FUSED && chirp_ok;
     p->stats.engine = p->engine;
     auto bail = [&](int code) {
         free_plan(p);
@@ -641,7 +656,7 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     sz = 0;
     r = ensure(&p->d_X, &sz, (size_t)max_batch * p->nh * 2 * p->esz);
     if (r != NW_OK) return bail(r);
-    if (p->engine == NW_ENGINE_FUSED && !p->large) {
+    if (p->engine == NW_ENGINE_FUSED && !p->large && !p->chirp) {
         e = nw::fused_prepare(n, dtype);
         if (e != hipSuccess) return bail(fail(NW_E_HIP, std::string("fused_prepare: ") + hipGetErrorString(e)));
     }

@@ -175,6 +175,14 @@ hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, 
                         int64_t nsig, hipStream_t s);
 hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 pi i j / n), cached per device
 
+// chirp-z engine (nw_chirp.hip): n not taken by the power-of-two kernels, 2n - 1 <= 16384
+// (fp32) / 8192 (fp64); one (scale, signal) row = two on-chip FFTs of M = 2^ceil(log2(2n-1))
+bool       chirp_supported(int64_t n, int dtype);
+size_t     chirp_wtable_bytes(int64_t n, int nfreq, int dtype, int kind);
+hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s);
+hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
+                        int64_t nsig, hipStream_t s);
+
 // two-pass engine for long signals (nw_large.hip): power-of-two 2^15 <= n <= 2^24, fp32 or
 // fp64.  scratch = Xt (n complex) + B (large_fchunk scales x n complex); support = kmax[nfreq]
 // + the fp64 column-pass twiddle tables.

@@ -1,0 +1,109 @@
+"""GPU parity of the chirp-z fused form (nw_chirp.hip): the lengths the power-of-two
+kernels do not take (any n with 2n - 1 <= 16384 in fp32, <= 8192 in fp64, other than the
+power-of-two n >= 1024) -- e.g. MNE epochs of 1201 or 4097 samples -- now run as two
+on-chip FFTs of M = 2^ceil(log2(2n - 1)) per (scale, signal) row instead of rocFFT.
+
+Tolerances against the fp64 oracle (numpy + scipy.fftpack, the reference's arithmetic):
+fp64 1e-12 of max|ref| (|.|^2 twice that), fp32 2e-5 (the chirp factors and two M-point
+FFTs add round-off over the power-of-two kernels' 1e-5; |.|^2 twice that), plus the 1e-30
+floor for outputs below fp32 range (test_gpu_parity.py).
+"""
+import numpy as np
+import pytest
+
+from oracle import nw_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import ninwavelets_amd as nw  # noqa: E402
+from ninwavelets_amd import _lib as L  # noqa: E402
+
+
+def synth(S, n, seed, sfreq=1000.):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / sfreq
+    fc = rng.uniform(1, 100, (S, 1))
+    ph = rng.uniform(0, 2 * np.pi, (S, 1))
+    return (np.sin(2 * np.pi * fc * t + ph) + 0.1 * rng.standard_normal((S, n))).astype(np.float32)
+
+
+def within(got, ref, dtype, out):
+    t = (1e-12 if dtype == 'float64' else 2e-5) * (2 if out == 'power' else 1)
+    floor = 1e-30 if dtype == 'float32' else 0.0
+    return np.max(np.abs(got - ref), initial=0.0) <= t * np.max(np.abs(ref), initial=0.0) + floor
+
+
+def oracle(kind, x, freqs, out, **kw):
+    y = np.stack([O.cwt(kind, xi.astype(np.float64), freqs, **kw) for xi in x])
+    return y if out == 'cwt' else (np.abs(y) if out == 'abs' else np.abs(y) ** 2)
+
+
+def chirp_plan(n, F, dtype, kind, params, freqs, max_batch=4, interpolate=False, engine=None):
+    g = L.trans_grid(n / 1000., 1000., interpolate)
+    p = nw.Plan(n, F, dtype, max_batch=max_batch, interpolate=interpolate, engine=engine)
+    p.set_wavelet(kind, list(params), np.asarray(freqs, dtype=np.float64), g)
+    return p
+
+
+F32_N = [1, 2, 3, 5, 21, 300, 301, 512, 1000, 1021, 1201, 2049, 3001, 4097, 8191]
+F64_N = [1, 3, 21, 300, 301, 1000, 1201, 2049, 4095]
+
+
+@pytest.mark.parametrize('dtype,n', [('float32', n) for n in F32_N] + [('float64', n) for n in F64_N])
+def test_chirp_lengths_against_oracle(dtype, n):
+    freqs = np.array([1.5, 7., 30., 120.])
+    S = 3
+    x = synth(S, n, 51 + n).astype(dtype)
+    p = chirp_plan(n, len(freqs), dtype, 'morse', (17.5, 3.), freqs)
+    for out in ('cwt', 'abs', 'power'):
+        got = p.execute(x, out_kind=out)
+        ref = oracle('morse', x, freqs, out)
+        assert within(got, ref, dtype, out), (out, np.max(np.abs(got - ref)) / np.max(np.abs(ref)))
+    st = p.stats()
+    assert st['engine'] == 'fused' and st['launches_fused'] == 3 * 1 and st['launches_multiply'] == 0
+
+
+@pytest.mark.parametrize('dtype', ['float32', 'float64'])
+def test_chirp_kinds_interpolate_and_chunks(dtype):
+    """Morlet, Shannon, MexicanHat (complex table rows), interpolate, several chunks
+    with a ragged last one, against the oracle and the rocFFT engine."""
+    n, S = 1201, 11
+    x = synth(S, n, 52).astype(dtype)
+    freqs = np.array([2., 9., 40., 90., 200.])
+    for kind, params, kw in (('morlet', (7., 0.), {'sigma': 7., 'gabor': False}), ('shannon', (), {})):
+        for interp in (False, True):
+            p = chirp_plan(n, len(freqs), dtype, kind, params, freqs, max_batch=4, interpolate=interp)
+            got = p.execute(x, out_kind='cwt')
+            ref = oracle(kind, x, freqs, 'cwt', interpolate=interp, **kw)
+            assert within(got, ref, dtype, 'cwt'), (kind, interp)
+            r = chirp_plan(n, len(freqs), dtype, kind, params, freqs, max_batch=4, interpolate=interp,
+                           engine='rocfft').execute(x, out_kind='cwt')
+            assert within(got, r.astype(np.complex128), dtype, 'cwt')
+    w = nw.MexicanHat(1000, dtype=dtype)
+    got = w.cwt(x[0].astype(np.float64 if dtype == 'float64' else np.float32), list(freqs))
+    ref = O.cwt('mexican_hat', x[0].astype(np.float64), list(freqs))
+    assert within(got, ref, dtype, 'cwt')
+
+
+@pytest.mark.parametrize('out', ['power_mean', 'itc'])
+def test_chirp_epoch_reductions(out):
+    n, S = 1201, 9
+    x = synth(S, n, 53)
+    freqs = np.array([3., 11., 60.])
+    p = chirp_plan(n, 3, 'float32', 'morse', (17.5, 3.), freqs, max_batch=4)
+    c = oracle('morse', x, freqs, 'cwt')
+    ref = np.mean(np.abs(c) ** 2, axis=0) if out == 'power_mean' else np.abs(np.mean(c / np.abs(c), axis=0))
+    got = p.execute(x, out_kind=out)
+    assert np.max(np.abs(got - ref)) <= 4e-5 * np.max(np.abs(ref))
+
+
+def test_no_chirp_flag_keeps_rocfft():
+    g = L.trans_grid(1.201, 1000., False)
+    import ctypes
+    h = ctypes.c_void_p()
+    L.check(L.lib().nw_plan_create(ctypes.byref(h), 0, 1201, 1, 2, L.NW_F32, L.NW_NO_CHIRP))
+    st = L.nw_stats()
+    L.check(L.lib().nw_plan_stats(h, ctypes.byref(st)))
+    assert st.engine == L.NW_ENGINE_ROCFFT
+    L.check(L.lib().nw_plan_destroy(h))
+    assert g.len_full >= 1201

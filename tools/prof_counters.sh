@@ -9,7 +9,7 @@ i=0
 while read -r grp; do
   [ -z "$grp" ] && continue
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --kernel-include-regex 'nw_fused|k1_multiply|cols_kernel|rows_kernel' --pmc $grp -d $out/p$i -o pmc --output-format csv -- python3 bench.py "$@" > $out/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --kernel-include-regex "${KREGEX:-nw_fused|k1_multiply|cols_kernel|rows_kernel}" --pmc $grp -d $out/p$i -o pmc --output-format csv -- python3 bench.py "$@" > $out/p$i.log 2>&1
   rc=$?; echo "pass $i ($grp) rc=$rc"
   if [ $rc -ne 0 ]; then tail -5 $out/p$i.log; exit $rc; fi
 done <<'GROUPS'
