@@ -27,19 +27,27 @@ constexpr int kGroupC = 8;    // signals per block
 constexpr int kTileFC = 8;    // scales per XCD tile
 constexpr int kTileGC = 4;    // signal groups per XCD tile
 constexpr int kRegOsz = 16;   // PassInfo without last-pass pairing: j = t + q*T everywhere
+#ifndef NW_CHIRP_PAIR
+#define NW_CHIRP_PAIR 0       // fp32 analytic rows, two signals per lane value (C2<f2>): measured
+                              // +-2 % at n = 700 / 1000 / 1201 (not VALU-bound), so off
+#endif
+#ifndef NW_CHIRP_PAIR_MAXM
+#define NW_CHIRP_PAIR_MAXM 4096   // pair kernels up to this M (2 waves/SIMD; 44-56 B scratch at 4096)
+#endif
 
 // exchange P-1 -> P and pass P, as passes_from (nw_fft_dev.h) without the stores: the
 // last pass leaves its outputs in registers, v[q*R + i] = output j + bitrev(i)*NS, j = t + q*T
 template <typename T, int N, int E, int P>
-__device__ __forceinline__ void passes_regs(C2<T>* v, T* lds, int t, const C2<T>* __restrict__ tw) {
+__device__ __forceinline__ void passes_regs(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw) {
+    using S = Sc<T>;   // T = f2: two signals per lane value, twiddles shared
     using I = PassInfo<N, E, P, kRegOsz>;
     if constexpr (P < Geometry<N, E>::npass()) {
         constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
         constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;
-        C2<T> pb[Q][LR > 0 ? LR : 1];
+        C2<S> pb[Q][LR > 0 ? LR : 1];
         if constexpr (!TABLED) {
 #pragma unroll
-            for (int q = 0; q < Q; ++q) twiddle_bases<T, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
+            for (int q = 0; q < Q; ++q) twiddle_bases<S, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
         }
         lds_barrier();
         lds_write<T, N, E, P - 1, 0>(v, lds, t);
@@ -52,7 +60,7 @@ __device__ __forceinline__ void passes_regs(C2<T>* v, T* lds, int t, const C2<T>
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
             if constexpr (TABLED) {
-                const C2<T>* tab = Tab1<T, N, E>::table(lds) + I::bfly(t, q) % I::NS;
+                const C2<S>* tab = Tab1<T, N, E>::table(lds) + I::bfly(t, q) % I::NS;
 #pragma unroll
                 for (int r = 1; r < R; ++r) v[q * R + r] = cmul(v[q * R + r], tab[(r - 1) * I::NS]);
             } else {
@@ -172,6 +180,93 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M>)) void nw_chirp_kernel(
     }
 }
 
+// Signal pairs (fp32, analytic real W rows), as nw_fused_pair_kernel: every lane value is
+// a C2<f2> holding signal s in the low and s+1 in the high half, so each butterfly, twiddle
+// multiply, chirp / Bh multiply and LDS access of both transforms serves two signals
+// (v_pk_* math, 8-B image slots); an odd last signal transforms a duplicate, not stored.
+template <int M, int E, int OUT>
+__global__ __launch_bounds__(M / E, 2) void nw_chirp_pair_kernel(
+    WDesc d, const cplx<float>* __restrict__ X, const float* __restrict__ wtab, void* __restrict__ out,
+    const C2<float>* __restrict__ tw, const C2<float>* __restrict__ bh, int64_t nsig, int nsg_pad) {
+    using G = Geometry<M, E>;
+    constexpr int TT = G::T;
+    constexpr int LP = G::npass() - 1;
+    using IL = PassInfo<M, E, LP, kRegOsz>;
+    static_assert(PassInfo<M, E, 1, kRegOsz>::R == E, "pass 1 must be radix E (pass-0 layout reads)");
+    using O = typename OutT<OUT, float>::type;
+    extern __shared__ __align__(16) unsigned char smem[];
+    f2* lds = reinterpret_cast<f2*>(smem);
+    const int t = threadIdx.x;
+    const int b = blockIdx.x;
+    const int xcd = b & 7;
+    const int local = b >> 3;
+    const int pos = local % (kTileFC * kTileGC);
+    const int round = local / (kTileFC * kTileGC);
+    const int nfr = (d.nfreq + kTileFC - 1) / kTileFC;
+    const int fi = (round % nfr) * kTileFC + pos % kTileFC;
+    const int sg = ((round / nfr) * kTileGC + pos / kTileFC) * 8 + xcd;
+    if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * kGroupC >= nsig) return;
+    const int64_t s_begin = (int64_t)sg * kGroupC;
+    const int64_t s_end = min(nsig, s_begin + kGroupC);
+
+    const int n = (int)d.n;
+    const uint32_t n2 = 2u * (uint32_t)n;
+    const float inv_n2 = 1.0f / (float)n2;
+    const float* wrow = wtab + (int64_t)fi * n;
+    Tab1<f2, M, E>::fill(lds, tw, t);
+    for (int64_t s = s_begin; s < s_end; s += 2) {
+        const bool two = s + 1 < s_end;
+        const cplx<float>* X0 = X + s * d.nh;
+        const cplx<float>* X1 = X + (two ? s + 1 : s) * d.nh;
+        C2<f2> v[E];
+#pragma unroll
+        for (int r = 0; r < E; ++r) {
+            const int k = t + r * TT;
+            C2<f2> a{f2{0.f, 0.f}, f2{0.f, 0.f}};
+            if (k < n) {
+                const float w = wrow[k];
+                const cplx<float> x0 = spectrum_bin<float>(X0, d, k), x1 = spectrum_bin<float>(X1, d, k);
+                a = cmul(C2<f2>{f2{w * x0.re, w * x1.re}, f2{w * x0.im, w * x1.im}},
+                         chirp<float>(k, n2, inv_n2, nullptr));
+            }
+            v[r] = C2<f2>{a.re, -a.im};
+        }
+        idft_br<f2, E, E / 2>(v);
+        passes_regs<f2, M, E, 1>(v, lds, t, tw);
+#pragma unroll
+        for (int q = 0; q < IL::Q; ++q)
+#pragma unroll
+            for (int i = 0; i < IL::R; ++i) {
+                const int m = t + q * TT + bitrev<IL::R>(i) * IL::NS;
+                C2<f2>& e = v[q * IL::R + i];
+                e = cmul(C2<f2>{e.re, -e.im}, bh[m]);
+            }
+        lds_barrier();
+        lds_write<f2, M, E, LP, 0>(v, lds, t);
+        lds_barrier();
+        lds_read<f2, M, E, 1, 0, kRegOsz>(v, lds, t);
+        lds_barrier();
+        lds_write<f2, M, E, LP, 1>(v, lds, t);
+        lds_barrier();
+        lds_read<f2, M, E, 1, 1, kRegOsz>(v, lds, t);
+        idft_br<f2, E>(v);
+        passes_regs<f2, M, E, 1>(v, lds, t, tw);
+        O* o0 = reinterpret_cast<O*>(out) + (s * d.nfreq + fi) * (int64_t)n;
+        O* o1 = reinterpret_cast<O*>(out) + ((s + 1) * d.nfreq + fi) * (int64_t)n;
+#pragma unroll
+        for (int q = 0; q < IL::Q; ++q)
+#pragma unroll
+            for (int i = 0; i < IL::R; ++i) {
+                const int idx = t + q * TT + bitrev<IL::R>(i) * IL::NS;
+                if (idx < n) {
+                    const C2<f2> y = cmul(v[q * IL::R + i], chirp<float>(idx, n2, inv_n2, nullptr));
+                    o0[idx] = out_value<OUT, float>(lo(y));
+                    if (two) o1[idx] = out_value<OUT, float>(hi(y));
+                }
+            }
+    }
+}
+
 // W rows of length n (1/n folded in) for the chirp engine: the reference's cached row,
 // pad_to'd (base.py:75-82, 396-397); X's interpolate mask is applied by spectrum_bin
 template <typename T, bool REALW>
@@ -280,6 +375,20 @@ hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wta
         kern<<<(unsigned)blocks, threads, lds, s>>>(d, Xc, wtab, out, twc, bh, ct, nsig, (int)nsg_pad);
         e = hipGetLastError();
     };
+    if constexpr (std::is_same<T, float>::value && REALW && NW_CHIRP_PAIR && E <= 16 && M <= NW_CHIRP_PAIR_MAXM) {
+        const int lp = kLdsBytes<f2, M, E>;
+        const float* wt = reinterpret_cast<const float*>(wtab);
+        auto gp = [&](auto kern) {
+            e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lp);
+            if (e != hipSuccess) return;
+            kern<<<(unsigned)blocks, threads, lp, s>>>(d, Xc, wt, out, twc, bh, nsig, (int)nsg_pad);
+            e = hipGetLastError();
+        };
+        if (out_kind == NW_OUT_CWT) gp(nw_chirp_pair_kernel<M, E, NW_OUT_CWT>);
+        else if (out_kind == NW_OUT_POWER) gp(nw_chirp_pair_kernel<M, E, NW_OUT_POWER>);
+        else gp(nw_chirp_pair_kernel<M, E, NW_OUT_ABS>);
+        return e;
+    }
     if (out_kind == NW_OUT_CWT) go(nw_chirp_kernel<T, M, E, NW_OUT_CWT, REALW>);
     else if (out_kind == NW_OUT_POWER) go(nw_chirp_kernel<T, M, E, NW_OUT_POWER, REALW>);
     else go(nw_chirp_kernel<T, M, E, NW_OUT_ABS, REALW>);
