@@ -98,9 +98,9 @@ template <typename T> struct WRow<T, false> {
 // waves per SIMD without scratch (tools/regs.py): fp32 M <= 4096 fit 168 VGPRs (3 waves;
 // 4 spilled 44 B at M = 1024), M >= 8192 and fp64 need up to 256 (2 waves; fp32 M = 16384
 // at E = 32 still spills ~230 B there)
-template <typename T, int M> constexpr int kChirpWps = (sizeof(T) == 4 && M <= 4096) ? 3 : 2;
+template <typename T, int M, int E> constexpr int kChirpWps = E <= 8 ? 4 : (sizeof(T) == 4 && M <= 4096) ? 3 : 2;
 template <typename T, int M, int E, int OUT, bool REALW>
-__global__ __launch_bounds__(M / E, (kChirpWps<T, M>)) void nw_chirp_kernel(
+__global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     WDesc d, const cplx<T>* __restrict__ X, const void* __restrict__ wtab, void* __restrict__ out,
     const C2<T>* __restrict__ tw, const C2<T>* __restrict__ bh, const C2<T>* __restrict__ ct, int64_t nsig,
     int nsg_pad) {
@@ -398,8 +398,12 @@ hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wta
 }  // namespace
 
 // (dtype, M, E) of the chirp engine: fp32 M <= 16384 (E = 32 at 16384), fp64 M <= 8192
+#ifndef NW_CHIRP_E
+#define NW_CHIRP_E 16   // elements per thread, fp32 M <= 8192
+#endif
 #define NW_CHIRP_TABLE(X)                                                                        \
-    X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, 16) X(float, 8192, 16) X(float, 16384, 32) \
+    X(float, 1024, NW_CHIRP_E) X(float, 2048, NW_CHIRP_E) X(float, 4096, NW_CHIRP_E)             \
+    X(float, 8192, NW_CHIRP_E) X(float, 16384, 32)                                               \
     X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) X(double, 8192, 16)
 
 bool chirp_supported(int64_t n, int dtype) {
