@@ -122,6 +122,7 @@ struct nw_plan {
     bool wtab_valid = false;
     bool large = false;              // fused engine, two-pass form (nw_large.hip)
     bool chirp = false;              // fused engine, chirp-z form (nw_chirp.hip): other n
+    int64_t chirp_counts[5] = {0, 0, 0, 0, 0};   // rows per M class (M = 1024 << c)
     void* d_scratch = nullptr;       // two-pass form: Xt + B
     size_t d_scratch_bytes = 0;
 
@@ -324,11 +325,11 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
         // chirp-z form (any other n up to 8192 fp32 / 4096 fp64): two on-chip FFTs per row
         if (!p->wtab_valid) {
             NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes, nw::chirp_wtable_bytes(p->n, p->nfreq, p->dtype, p->desc.kind)));
-            NW_HIP(nw::build_chirp_wtable(p->desc, p->dtype, p->d_wtab, p->stream));
+            NW_HIP(nw::build_chirp_wtable(p->desc, p->dtype, p->d_wtab, p->stream, p->chirp_counts));
             p->wtab_valid = true;
         }
         return staged(p, ST_FUSED, [&] {
-            NW_HIP(nw::launch_chirp(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->stream));
+            NW_HIP(nw::launch_chirp(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->chirp_counts, p->stream));
             return NW_OK;
         });
     }

@@ -17,6 +17,8 @@
 #include <map>
 #include <mutex>
 #include <tuple>
+#include <vector>
+#include <algorithm>
 
 #include "nw_fft_dev.h"
 
@@ -27,13 +29,6 @@ constexpr int kGroupC = 8;    // signals per block
 constexpr int kTileFC = 8;    // scales per XCD tile
 constexpr int kTileGC = 4;    // signal groups per XCD tile
 constexpr int kRegOsz = 16;   // PassInfo without last-pass pairing: j = t + q*T everywhere
-#ifndef NW_CHIRP_PAIR
-#define NW_CHIRP_PAIR 0       // fp32 analytic rows, two signals per lane value (C2<f2>): measured
-                              // +-2 % at n = 700 / 1000 / 1201 (not VALU-bound), so off
-#endif
-#ifndef NW_CHIRP_PAIR_MAXM
-#define NW_CHIRP_PAIR_MAXM 4096   // pair kernels up to this M (2 waves/SIMD; 44-56 B scratch at 4096)
-#endif
 
 // exchange P-1 -> P and pass P, as passes_from (nw_fft_dev.h) without the stores: the
 // last pass leaves its outputs in registers, v[q*R + i] = output j + bitrev(i)*NS, j = t + q*T
@@ -103,7 +98,7 @@ template <typename T, int M, int E, int OUT, bool REALW>
 __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     WDesc d, const cplx<T>* __restrict__ X, const void* __restrict__ wtab, void* __restrict__ out,
     const C2<T>* __restrict__ tw, const C2<T>* __restrict__ bh, const C2<T>* __restrict__ ct, int64_t nsig,
-    int nsg_pad) {
+    int nsg_pad, const int* __restrict__ rowmap, int nrows) {
     using G = Geometry<M, E>;
     constexpr int TT = G::T;
     constexpr int LP = G::npass() - 1;
@@ -120,10 +115,11 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     const int local = b >> 3;
     const int pos = local % (kTileFC * kTileGC);
     const int round = local / (kTileFC * kTileGC);
-    const int nfr = (d.nfreq + kTileFC - 1) / kTileFC;
-    const int fi = (round % nfr) * kTileFC + pos % kTileFC;
+    const int nfr = (nrows + kTileFC - 1) / kTileFC;
+    const int fl = (round % nfr) * kTileFC + pos % kTileFC;   // this launch's rows: rowmap[0 .. nrows)
     const int sg = ((round / nfr) * kTileGC + pos / kTileFC) * 8 + xcd;
-    if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * kGroupC >= nsig) return;
+    if (fl >= nrows || sg >= nsg_pad || (int64_t)sg * kGroupC >= nsig) return;
+    const int fi = rowmap[fl];
     const int64_t s_begin = (int64_t)sg * kGroupC;
     const int64_t s_end = min(nsig, s_begin + kGroupC);
 
@@ -180,93 +176,6 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     }
 }
 
-// Signal pairs (fp32, analytic real W rows), as nw_fused_pair_kernel: every lane value is
-// a C2<f2> holding signal s in the low and s+1 in the high half, so each butterfly, twiddle
-// multiply, chirp / Bh multiply and LDS access of both transforms serves two signals
-// (v_pk_* math, 8-B image slots); an odd last signal transforms a duplicate, not stored.
-template <int M, int E, int OUT>
-__global__ __launch_bounds__(M / E, 2) void nw_chirp_pair_kernel(
-    WDesc d, const cplx<float>* __restrict__ X, const float* __restrict__ wtab, void* __restrict__ out,
-    const C2<float>* __restrict__ tw, const C2<float>* __restrict__ bh, int64_t nsig, int nsg_pad) {
-    using G = Geometry<M, E>;
-    constexpr int TT = G::T;
-    constexpr int LP = G::npass() - 1;
-    using IL = PassInfo<M, E, LP, kRegOsz>;
-    static_assert(PassInfo<M, E, 1, kRegOsz>::R == E, "pass 1 must be radix E (pass-0 layout reads)");
-    using O = typename OutT<OUT, float>::type;
-    extern __shared__ __align__(16) unsigned char smem[];
-    f2* lds = reinterpret_cast<f2*>(smem);
-    const int t = threadIdx.x;
-    const int b = blockIdx.x;
-    const int xcd = b & 7;
-    const int local = b >> 3;
-    const int pos = local % (kTileFC * kTileGC);
-    const int round = local / (kTileFC * kTileGC);
-    const int nfr = (d.nfreq + kTileFC - 1) / kTileFC;
-    const int fi = (round % nfr) * kTileFC + pos % kTileFC;
-    const int sg = ((round / nfr) * kTileGC + pos / kTileFC) * 8 + xcd;
-    if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * kGroupC >= nsig) return;
-    const int64_t s_begin = (int64_t)sg * kGroupC;
-    const int64_t s_end = min(nsig, s_begin + kGroupC);
-
-    const int n = (int)d.n;
-    const uint32_t n2 = 2u * (uint32_t)n;
-    const float inv_n2 = 1.0f / (float)n2;
-    const float* wrow = wtab + (int64_t)fi * n;
-    Tab1<f2, M, E>::fill(lds, tw, t);
-    for (int64_t s = s_begin; s < s_end; s += 2) {
-        const bool two = s + 1 < s_end;
-        const cplx<float>* X0 = X + s * d.nh;
-        const cplx<float>* X1 = X + (two ? s + 1 : s) * d.nh;
-        C2<f2> v[E];
-#pragma unroll
-        for (int r = 0; r < E; ++r) {
-            const int k = t + r * TT;
-            C2<f2> a{f2{0.f, 0.f}, f2{0.f, 0.f}};
-            if (k < n) {
-                const float w = wrow[k];
-                const cplx<float> x0 = spectrum_bin<float>(X0, d, k), x1 = spectrum_bin<float>(X1, d, k);
-                a = cmul(C2<f2>{f2{w * x0.re, w * x1.re}, f2{w * x0.im, w * x1.im}},
-                         chirp<float>(k, n2, inv_n2, nullptr));
-            }
-            v[r] = C2<f2>{a.re, -a.im};
-        }
-        idft_br<f2, E, E / 2>(v);
-        passes_regs<f2, M, E, 1>(v, lds, t, tw);
-#pragma unroll
-        for (int q = 0; q < IL::Q; ++q)
-#pragma unroll
-            for (int i = 0; i < IL::R; ++i) {
-                const int m = t + q * TT + bitrev<IL::R>(i) * IL::NS;
-                C2<f2>& e = v[q * IL::R + i];
-                e = cmul(C2<f2>{e.re, -e.im}, bh[m]);
-            }
-        lds_barrier();
-        lds_write<f2, M, E, LP, 0>(v, lds, t);
-        lds_barrier();
-        lds_read<f2, M, E, 1, 0, kRegOsz>(v, lds, t);
-        lds_barrier();
-        lds_write<f2, M, E, LP, 1>(v, lds, t);
-        lds_barrier();
-        lds_read<f2, M, E, 1, 1, kRegOsz>(v, lds, t);
-        idft_br<f2, E>(v);
-        passes_regs<f2, M, E, 1>(v, lds, t, tw);
-        O* o0 = reinterpret_cast<O*>(out) + (s * d.nfreq + fi) * (int64_t)n;
-        O* o1 = reinterpret_cast<O*>(out) + ((s + 1) * d.nfreq + fi) * (int64_t)n;
-#pragma unroll
-        for (int q = 0; q < IL::Q; ++q)
-#pragma unroll
-            for (int i = 0; i < IL::R; ++i) {
-                const int idx = t + q * TT + bitrev<IL::R>(i) * IL::NS;
-                if (idx < n) {
-                    const C2<f2> y = cmul(v[q * IL::R + i], chirp<float>(idx, n2, inv_n2, nullptr));
-                    o0[idx] = out_value<OUT, float>(lo(y));
-                    if (two) o1[idx] = out_value<OUT, float>(hi(y));
-                }
-            }
-    }
-}
-
 // W rows of length n (1/n folded in) for the chirp engine: the reference's cached row,
 // pad_to'd (base.py:75-82, 396-397); X's interpolate mask is applied by spectrum_bin
 template <typename T, bool REALW>
@@ -281,90 +190,129 @@ __global__ __launch_bounds__(256) void chirp_wtable_kernel(WDesc d, void* wtab) 
         reinterpret_cast<C2<T>*>(wtab)[(int64_t)fi * d.n + k] = C2<T>{w.re, w.im};
 }
 
-// Bh[m] = (1/M) sum_j b[j] exp(-2 pi i m j / M) with b symmetric (b[M-j] = b[j]), in fp64:
-// (1/M) sum_{j<n} b[j] w_j cos(2 pi m j / M), w_0 = 1, w_j = 2; b[j] = exp(-i pi (j^2 mod 2n) / n)
-template <typename T>
-__global__ __launch_bounds__(256) void chirp_bhat_kernel(C2<T>* bh, C2<T>* ct, int n, int m_len) {
-    const int m = blockIdx.x * 256 + threadIdx.x;
-    if (m < n && ct) {
-        double s, c;
-        sincospi((double)(((int64_t)m * m) % (2 * (int64_t)n)) / n, &s, &c);
-        ct[m] = C2<T>{(T)c, (T)s};
+// Support of each W row: ksup[f] = last nonzero bin + 1 (0 for an all-zero row)
+template <typename T, bool REALW>
+__global__ __launch_bounds__(256) void chirp_support_kernel(const void* wtab, int64_t n, int* ksup) {
+    __shared__ int kmax[256];
+    const int fi = blockIdx.x;
+    int m = -1;
+    for (int64_t k = threadIdx.x; k < n; k += 256) {
+        bool nzv;
+        if constexpr (REALW) nzv = reinterpret_cast<const T*>(wtab)[(int64_t)fi * n + k] != T(0);
+        else {
+            const C2<T> w = reinterpret_cast<const C2<T>*>(wtab)[(int64_t)fi * n + k];
+            nzv = w.re != T(0) || w.im != T(0);
+        }
+        if (nzv) m = (int)k;
     }
+    kmax[threadIdx.x] = m;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) kmax[threadIdx.x] = max(kmax[threadIdx.x], kmax[threadIdx.x + w]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) ksup[fi] = kmax[0] + 1;
+}
+
+// Bh[m] = (1/M) sum_p b(p) exp(-2 pi i m p / M), in fp64, b(p) = exp(-i pi j^2 / n) for the
+// lag j = p (p < n) or p - M (p >= n) when -n < j < n, else 0.  With M >= 2n - 1 that is the
+// whole chirp; a row whose W support is K bins needs only the lags -K < j < n, so any
+// M >= n + K - 1 is wrap-free for it (the circular convolution equals the linear one on the
+// n outputs) -- the smaller M of band-limited rows.
+template <typename T>
+__global__ __launch_bounds__(256) void chirp_bhat_kernel(C2<T>* bh, int n, int m_len) {
+    const int m = blockIdx.x * 256 + threadIdx.x;
     if (m >= m_len) return;
     double re = 0.0, im = 0.0;
-    for (int j = 0; j < n; ++j) {
-        double bs, bc;
-        sincospi(-(double)(((int64_t)j * j) % (2 * (int64_t)n)) / n, &bs, &bc);
-        const double cw = cospi(2.0 * (double)(((int64_t)m * j) % m_len) / m_len) * (j == 0 ? 1.0 : 2.0);
-        re += bc * cw;
-        im += bs * cw;
+    for (int p = 0; p < m_len; ++p) {
+        const int j = p < n ? p : p - m_len;
+        if (j <= -n) continue;
+        const int64_t aj = j < 0 ? -(int64_t)j : j;
+        double bs, bc, es, ec;
+        sincospi(-(double)((aj * aj) % (2 * (int64_t)n)) / n, &bs, &bc);
+        sincospi(-2.0 * (double)(((int64_t)m * p) % m_len) / m_len, &es, &ec);
+        re += bc * ec - bs * es;
+        im += bc * es + bs * ec;
     }
     bh[m] = C2<T>{(T)(re / m_len), (T)(im / m_len)};
 }
 
+// the fp64 chirp c(k) = exp(+i pi k^2 / n), k < n
+template <typename T>
+__global__ __launch_bounds__(256) void chirp_ct_kernel(C2<T>* ct, int n) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= n) return;
+    double sn, cs;
+    sincospi((double)(((int64_t)k * k) % (2 * (int64_t)n)) / n, &sn, &cs);
+    ct[k] = C2<T>{(T)cs, (T)sn};
+}
+
 struct ChirpKey {
     int dev;
-    int64_t n;
+    int64_t n, m;
     int dtype;
-    bool operator<(const ChirpKey& o) const { return std::tie(dev, n, dtype) < std::tie(o.dev, o.n, o.dtype); }
+    bool operator<(const ChirpKey& o) const {
+        return std::tie(dev, n, m, dtype) < std::tie(o.dev, o.n, o.m, o.dtype);
+    }
 };
 std::mutex g_chirp_mu;
-std::map<ChirpKey, void*> g_chirp;   // Bh[M] then (fp64) c[n], per device and length
+std::map<ChirpKey, void*> g_chirp;   // per device, length and M: Bh[M] then (fp64) c[n]
 
+constexpr int kChirpClasses = 5;      // M = 1024 << c, c < 5
 int64_t chirp_m(int64_t n) {
     int64_t m = 1024;
     while (m < 2 * n - 1) m <<= 1;
     return m;
 }
 
-hipError_t chirp_tables(int64_t n, int dtype, void** out) {
+hipError_t chirp_tables(int64_t n, int64_t m, int dtype, void** out) {
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     std::lock_guard<std::mutex> lk(g_chirp_mu);
-    auto it = g_chirp.find({dev, n, dtype});
+    auto it = g_chirp.find({dev, n, m, dtype});
     if (it != g_chirp.end()) {
         *out = it->second;
         return hipSuccess;
     }
-    const int64_t m = chirp_m(n);
     const size_t esz = dtype == NW_F32 ? sizeof(C2<float>) : sizeof(C2<double>);
     void* p = nullptr;
     e = hipMalloc(&p, (size_t)(m + n) * esz);
     if (e != hipSuccess) return e;
-    const unsigned blocks = (unsigned)((m + 255) / 256);
-    if (dtype == NW_F32)
-        chirp_bhat_kernel<float><<<blocks, 256>>>((C2<float>*)p, (C2<float>*)p + m, (int)n, (int)m);
-    else
-        chirp_bhat_kernel<double><<<blocks, 256>>>((C2<double>*)p, (C2<double>*)p + m, (int)n, (int)m);
+    const unsigned bm = (unsigned)((m + 255) / 256), bn = (unsigned)((n + 255) / 256);
+    if (dtype == NW_F32) {
+        chirp_bhat_kernel<float><<<bm, 256>>>((C2<float>*)p, (int)n, (int)m);
+    } else {
+        chirp_bhat_kernel<double><<<bm, 256>>>((C2<double>*)p, (int)n, (int)m);
+        chirp_ct_kernel<double><<<bn, 256>>>((C2<double>*)p + m, (int)n);
+    }
     e = hipGetLastError();
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
         (void)hipFree(p);
         return e;
     }
-    g_chirp[{dev, n, dtype}] = p;
+    g_chirp[{dev, n, m, dtype}] = p;
     *out = p;
     return hipSuccess;
 }
 
 template <typename T, int M, int E, bool REALW>
 hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
-                    hipStream_t s) {
+                    const int* rowmap, int nrows, hipStream_t s) {
     constexpr int threads = M / E;
     const int lds = kLdsBytes<T, M, E>;
     void* tw = nullptr;
     hipError_t e = fused_twiddles(M, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
     void* tabs = nullptr;
-    e = chirp_tables(d.n, sizeof(T) == 4 ? NW_F32 : NW_F64, &tabs);
+    e = chirp_tables(d.n, M, sizeof(T) == 4 ? NW_F32 : NW_F64, &tabs);
     if (e != hipSuccess) return e;
     const C2<T>* bh = reinterpret_cast<const C2<T>*>(tabs);
     const C2<T>* ct = bh + M;
     const int64_t nsg = (nsig + kGroupC - 1) / kGroupC;
     const int64_t nsg_pad = (nsg + 8 * kTileGC - 1) / (8 * kTileGC) * (8 * kTileGC);
-    const int64_t nfr = (d.nfreq + kTileFC - 1) / kTileFC;
+    const int64_t nfr = (nrows + kTileFC - 1) / kTileFC;
     const int64_t blocks = nsg_pad * nfr * kTileFC;
     if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
     const cplx<T>* Xc = reinterpret_cast<const cplx<T>*>(X);
@@ -372,23 +320,9 @@ hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wta
     auto go = [&](auto kern) {
         e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return;
-        kern<<<(unsigned)blocks, threads, lds, s>>>(d, Xc, wtab, out, twc, bh, ct, nsig, (int)nsg_pad);
+        kern<<<(unsigned)blocks, threads, lds, s>>>(d, Xc, wtab, out, twc, bh, ct, nsig, (int)nsg_pad, rowmap, nrows);
         e = hipGetLastError();
     };
-    if constexpr (std::is_same<T, float>::value && REALW && NW_CHIRP_PAIR && E <= 16 && M <= NW_CHIRP_PAIR_MAXM) {
-        const int lp = kLdsBytes<f2, M, E>;
-        const float* wt = reinterpret_cast<const float*>(wtab);
-        auto gp = [&](auto kern) {
-            e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lp);
-            if (e != hipSuccess) return;
-            kern<<<(unsigned)blocks, threads, lp, s>>>(d, Xc, wt, out, twc, bh, nsig, (int)nsg_pad);
-            e = hipGetLastError();
-        };
-        if (out_kind == NW_OUT_CWT) gp(nw_chirp_pair_kernel<M, E, NW_OUT_CWT>);
-        else if (out_kind == NW_OUT_POWER) gp(nw_chirp_pair_kernel<M, E, NW_OUT_POWER>);
-        else gp(nw_chirp_pair_kernel<M, E, NW_OUT_ABS>);
-        return e;
-    }
     if (out_kind == NW_OUT_CWT) go(nw_chirp_kernel<T, M, E, NW_OUT_CWT, REALW>);
     else if (out_kind == NW_OUT_POWER) go(nw_chirp_kernel<T, M, E, NW_OUT_POWER, REALW>);
     else go(nw_chirp_kernel<T, M, E, NW_OUT_ABS, REALW>);
@@ -412,36 +346,81 @@ bool chirp_supported(int64_t n, int dtype) {
     return (dtype == NW_F32 || dtype == NW_F64) && 2 * n - 1 <= mmax;
 }
 
-size_t chirp_wtable_bytes(int64_t n, int nfreq, int dtype, int kind) {
+// table buffer: W rows, then ksup[nfreq], then the row map (rows grouped by M class)
+size_t chirp_w_bytes(int64_t n, int nfreq, int dtype, int kind) {
     const size_t esz = dtype == NW_F32 ? sizeof(float) : sizeof(double);
-    return (size_t)n * nfreq * esz * (kind != NW_TABLE ? 1 : 2);
+    return ((size_t)n * nfreq * esz * (kind != NW_TABLE ? 1 : 2) + 15) / 16 * 16;
+}
+size_t chirp_wtable_bytes(int64_t n, int nfreq, int dtype, int kind) {
+    return chirp_w_bytes(n, nfreq, dtype, kind) + 2 * (size_t)nfreq * sizeof(int);
 }
 
-hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
+hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts) {
     dim3 grid((unsigned)((d.n + 255) / 256), (unsigned)d.nfreq);
     const bool realw = d.kind != NW_TABLE;
+    int* ksup = reinterpret_cast<int*>(reinterpret_cast<char*>(wtab) + chirp_w_bytes(d.n, d.nfreq, dtype, d.kind));
+    int* rowmap = ksup + d.nfreq;
     if (dtype == NW_F32) {
         if (realw) chirp_wtable_kernel<float, true><<<grid, 256, 0, s>>>(d, wtab);
         else chirp_wtable_kernel<float, false><<<grid, 256, 0, s>>>(d, wtab);
+        if (realw) chirp_support_kernel<float, true><<<d.nfreq, 256, 0, s>>>(wtab, d.n, ksup);
+        else chirp_support_kernel<float, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, ksup);
     } else {
         if (realw) chirp_wtable_kernel<double, true><<<grid, 256, 0, s>>>(d, wtab);
         else chirp_wtable_kernel<double, false><<<grid, 256, 0, s>>>(d, wtab);
+        if (realw) chirp_support_kernel<double, true><<<d.nfreq, 256, 0, s>>>(wtab, d.n, ksup);
+        else chirp_support_kernel<double, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, ksup);
     }
-    return hipGetLastError();
+    hipError_t e = hipGetLastError();
+    // once per wavelet: the rows' M classes on the host (M >= n + K - 1 wrap-free, >= 2K for
+    // the pruned first pass 0, >= 1024, <= the full 2^ceil(log2(2n - 1)))
+    std::vector<int> ks(d.nfreq);
+    if (e == hipSuccess) e = hipMemcpyAsync(ks.data(), ksup, d.nfreq * sizeof(int), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return e;
+    const int64_t mfull = chirp_m(d.n);
+    std::vector<int> cls(d.nfreq);
+    for (int c = 0; c < kChirpClasses; ++c) counts[c] = 0;
+    for (int f = 0; f < d.nfreq; ++f) {
+        const int64_t need = std::max<int64_t>(d.n + std::max(ks[f], 1) - 1, 2 * (int64_t)ks[f]);
+        int64_t m = 1024;
+        while (m < need && m < mfull) m <<= 1;
+        int c = 0;
+        while ((1024ll << c) < m) ++c;
+        cls[f] = c;
+        counts[c]++;
+    }
+    std::vector<int> map;
+    for (int c = 0; c < kChirpClasses; ++c)
+        for (int f = 0; f < d.nfreq; ++f)
+            if (cls[f] == c) map.push_back(f);
+    e = hipMemcpyAsync(rowmap, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    return e;
 }
 
 hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
-                        int64_t nsig, hipStream_t s) {
+                        int64_t nsig, const int64_t* counts, hipStream_t s) {
     if (!chirp_supported(d.n, dtype)) return hipErrorNotSupported;
-    const int64_t m = chirp_m(d.n);
     const bool realw = d.kind != NW_TABLE;
-#define NW_CHIRP_LAUNCH(TY, MM, EE)                                                          \
-    if (m == MM && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64))                            \
-        return realw ? launch_m<TY, MM, EE, true>(d, out_kind, X, wtab, out, nsig, s)        \
-                     : launch_m<TY, MM, EE, false>(d, out_kind, X, wtab, out, nsig, s);
-    NW_CHIRP_TABLE(NW_CHIRP_LAUNCH)
+    const int* rowmap = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
+                                                     chirp_w_bytes(d.n, d.nfreq, dtype, d.kind)) + d.nfreq;
+    int64_t off = 0;
+    for (int c = 0; c < kChirpClasses; ++c) {
+        const int64_t cnt = counts[c];
+        if (cnt == 0) continue;
+        const int64_t m = 1024ll << c;
+        hipError_t e = hipErrorNotSupported;
+#define NW_CHIRP_LAUNCH(TY, MM, EE)                                                                             \
+        if (m == MM && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64))                                            \
+            e = realw ? launch_m<TY, MM, EE, true>(d, out_kind, X, wtab, out, nsig, rowmap + off, (int)cnt, s) \
+                      : launch_m<TY, MM, EE, false>(d, out_kind, X, wtab, out, nsig, rowmap + off, (int)cnt, s);
+        NW_CHIRP_TABLE(NW_CHIRP_LAUNCH)
 #undef NW_CHIRP_LAUNCH
-    return hipErrorNotSupported;
+        if (e != hipSuccess) return e;
+        off += cnt;
+    }
+    return hipSuccess;
 }
 
 }  // namespace nw

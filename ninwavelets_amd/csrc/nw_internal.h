@@ -179,9 +179,11 @@ hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 p
 // (fp32) / 8192 (fp64); one (scale, signal) row = two on-chip FFTs of M = 2^ceil(log2(2n-1))
 bool       chirp_supported(int64_t n, int dtype);
 size_t     chirp_wtable_bytes(int64_t n, int nfreq, int dtype, int kind);
-hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s);
+// builds W, each row's support and the rows grouped by M class (M = 1024 << c, c < 5:
+// counts[c] rows each; synchronises s once); launch_chirp runs one kernel per class
+hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts);
 hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
-                        int64_t nsig, hipStream_t s);
+                        int64_t nsig, const int64_t* counts, hipStream_t s);
 
 // two-pass engine for long signals (nw_large.hip): power-of-two 2^15 <= n <= 2^24, fp32 or
 // fp64.  scratch = Xt (n complex) + B (large_fchunk scales x n complex); support = kmax[nfreq]

@@ -1,7 +1,9 @@
 """GPU parity of the chirp-z fused form (nw_chirp.hip): the lengths the power-of-two
 kernels do not take (any n with 2n - 1 <= 16384 in fp32, <= 8192 in fp64, other than the
 power-of-two n >= 1024) -- e.g. MNE epochs of 1201 or 4097 samples -- now run as two
-on-chip FFTs of M = 2^ceil(log2(2n - 1)) per (scale, signal) row instead of rocFFT.
+on-chip FFTs per (scale, signal) row instead of rocFFT, of the smallest power of two M >= 1024
+that is wrap-free for the row (M >= n + K - 1, K = the W row's support; at most
+2^ceil(log2(2n - 1))).
 
 Tolerances against the fp64 oracle (numpy + scipy.fftpack, the reference's arithmetic):
 fp64 1e-12 of max|ref| (|.|^2 twice that), fp32 2e-5 (the chirp factors and two M-point
@@ -107,3 +109,27 @@ def test_no_chirp_flag_keeps_rocfft():
     assert st.engine == L.NW_ENGINE_ROCFFT
     L.check(L.lib().nw_plan_destroy(h))
     assert g.len_full >= 1201
+
+
+@pytest.mark.parametrize('dtype', ['float32', 'float64'])
+def test_chirp_rows_of_different_transform_sizes(dtype):
+    """Band-limited rows run at the smallest wrap-free M >= n + K - 1 (K = the W row's
+    support): interleaved low / high scales at n = 1201 fall into M = 2048 and 4096
+    launches of one execute; the full-M rows (K ~ n) and all-zero rows are covered too."""
+    n, S = 1201, 5
+    x = synth(S, n, 54).astype(dtype)
+    freqs = np.array([2., 300., 5., 450., 100., 20000.])   # 20 kHz: support beyond n/2
+    p = chirp_plan(n, len(freqs), dtype, 'morse', (17.5, 3.), freqs, max_batch=4)
+    for out in ('cwt', 'power'):
+        got = p.execute(x, out_kind=out)
+        ref = oracle('morse', x, freqs, out)
+        assert within(got, ref, dtype, out), out
+    tab = np.zeros((3, n), dtype=np.complex128)          # an all-zero table row among others
+    tab[1, :40] = 1.0 + 0.5j
+    tab[2] = np.exp(-np.arange(n) / 50.)
+    g = L.nw_grid(1.0, n, n)
+    q = nw.Plan(n, 3, dtype, max_batch=4)
+    q.set_wavelet('table', [], np.array([1., 2., 3.]), g, table=tab)
+    got = q.execute(x, out_kind='cwt')
+    ref = np.stack([O.cwt_from_rows(xi.astype(np.float64), list(tab), False) for xi in x])
+    assert within(got, ref, dtype, 'cwt')
