@@ -73,8 +73,15 @@ def test_trans_grid_rejects_bad_args():
 
 
 def test_fused_support_table():
-    assert L.fused_supported(300, L.NW_F32) is False        # non power of two -> rocFFT engine
-    assert L.fused_supported(512, L.NW_F64) is False        # below the smallest on-chip size
+    # every length up to 2n - 1 <= 16384 (fp32) / 8192 (fp64) has a fused form (the chirp-z
+    # form for non-powers of two and n < 1024); longer odd lengths stay on the rocFFT engine
+    for n in (1, 2, 3, 300, 512, 1201, 4097, 8192):
+        assert L.fused_supported(n, L.NW_F32) is True, n
+    for n in (1, 300, 512, 4095):
+        assert L.fused_supported(n, L.NW_F64) is True, n
+    assert L.fused_supported(8193, L.NW_F32) is False
+    assert L.fused_supported(4097, L.NW_F64) is False
+    assert L.fused_supported(20001, L.NW_F32) is False
     for dt in (L.NW_F32, L.NW_F64):
         for lg in range(10, 25):                             # one pass to 2^14, two passes above
             assert L.fused_supported(1 << lg, dt) is True, (lg, dt)
