@@ -158,9 +158,25 @@ template <int KIND> struct RowW<float, KIND> {
 
 // fp64: psi_f64 (the reference's expression order: pow / exp on nu = j * delta, nu / f)
 // times 1/n, exactly as wavelet_bin<double>, with the per-scale loads hoisted
+#ifndef NW_MORSE_IPOW
+#define NW_MORSE_IPOW 0   // measured: C5 fp64 rows 59.7 -> 93.8 ms/step (the N2 = 16384 Morse rows kernel
+                          // spills 76 B with it), so off
+#endif
+
+__device__ __forceinline__ double ipow(double x, int e) {   // x^e, e >= 0 (uniform e)
+    double acc = 1.0;
+    while (e) {
+        if (e & 1) acc *= x;
+        x *= x;
+        e >>= 1;
+    }
+    return acc;
+}
 template <int KIND> struct RowW<double, KIND> {
     double delta, f, peak, b, r, bor, sigma, cpi, kappa, scale;
     int off, lenv;
+    int bi, ri;       // Morse with 2b and r small integers (the default 17.5, 3): x^b and x^r
+    bool bhalf, ipw;  // by multiplications (+ one sqrt) and ONE exp -- no log, no second exp
     __device__ __forceinline__ void init(const WDesc& d, int fi) {
         delta = d.delta;
         f = d.freq ? d.freq[fi] : 1.0;
@@ -174,6 +190,11 @@ template <int KIND> struct RowW<double, KIND> {
         scale = d.scale;
         off = (int)d.off;
         lenv = d.len_valid < 0x7fffffff ? (int)d.len_valid : 0x7fffffff;
+        ipw = NW_MORSE_IPOW && b >= 0.0 && b <= 64.0 && 2.0 * b == rint(2.0 * b) && r >= 1.0 && r <= 8.0 &&
+              r == rint(r);
+        bi = ipw ? (int)floor(b) : 0;
+        bhalf = ipw && b - floor(b) == 0.5;
+        ri = ipw ? (int)r : 0;
     }
     __device__ __forceinline__ double operator()(int j) const {
         if ((unsigned)j >= (unsigned)lenv) return 0.0;
@@ -185,8 +206,18 @@ template <int KIND> struct RowW<double, KIND> {
             // support; psi(0) = 0 as np.heaviside(0, 0))
             const double x = nu / f;
             if (!(x > 0.0)) return 0.0;
-            const double lx = log(x);
-            psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
+            if (ipw) {
+                // 2 x^b e^{(b/r)(1 - x^r)}: a few ulp from pow (<< the 1e-12 tolerance); where
+                // x^b would overflow the exponential is already exactly 0
+                const double e = exp(bor * (1.0 - ipow(x, ri)));
+                if (e == 0.0) return 0.0;
+                double xb = ipow(x, bi);
+                if (bhalf) xb *= sqrt(x);
+                psi = 2.0 * xb * e;
+            } else {
+                const double lx = log(x);
+                psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
+            }
         } else if constexpr (KIND == NW_MORLET) {
             const double x = nu / f * peak;
             const double a = sigma - x;
