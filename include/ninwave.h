@@ -64,7 +64,8 @@ extern "C" {
 #define NW_TIMING        0x100u/* record HIP events around every stage (nw_plan_stats)            */
 #define NW_NO_CHIRP      0x400u/* auto engine: keep the rocFFT engine for lengths the chirp-z fused
                                   form would take (non-power-of-two n, 2n-1 <= 16384 fp32 /
-                                  8192 fp64, and n < 1024)                                     */
+                                  8192 fp64, and n < 1024; up to n < 16384 / 8192 when every
+                                  wavelet row's support K fits n + K - 1 <= 16384 / 8192)      */
 #define NW_NO_DEDUP      0x200u/* compute every scale row even when wavelet rows repeat (by
                                   default rows with identical W -- Shannon ignores f
                                   (wavelets.py:256-262), repeated freqs -- are computed once

@@ -123,6 +123,8 @@ struct nw_plan {
     bool large = false;              // fused engine, two-pass form (nw_large.hip)
     bool chirp = false;              // fused engine, chirp-z form (nw_chirp.hip): other n
     int64_t chirp_counts[5] = {0, 0, 0, 0, 0};   // rows per M class (M = 1024 << c)
+    bool chirp_tentative = false;    // auto engine, 2n - 1 > M_max: chirp-z only if every row's
+                                     // support fits (checked when the table is built), else rocFFT
     void* d_scratch = nullptr;       // two-pass form: Xt + B
     size_t d_scratch_bytes = 0;
 
@@ -275,8 +277,28 @@ int run_fft_rows(nw_plan* p, bool inverse, int64_t rows, char* in, char* out, si
     return NW_OK;
 }
 
+// The chirp-z table (W rows, supports, rows grouped by M) of the current wavelet.  A
+// tentative length (2n - 1 > M_max) whose rows do not all fit switches the plan to the
+// rocFFT engine until the next nw_plan_set_wavelet.
+int chirp_table(nw_plan* p) {
+    if (p->wtab_valid) return NW_OK;
+    NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes, nw::chirp_wtable_bytes(p->n, p->nfreq, p->dtype, p->desc.kind)));
+    bool fits = true;
+    NW_HIP(nw::build_chirp_wtable(p->desc, p->dtype, p->d_wtab, p->stream, p->chirp_counts, &fits));
+    if (!fits) {
+        if (!p->chirp_tentative)
+            return fail(NW_E_INVALID, "chirp-z form: a wavelet row is wider than the largest on-chip transform");
+        p->chirp = false;
+        p->engine = NW_ENGINE_ROCFFT;
+        p->stats.engine = NW_ENGINE_ROCFFT;
+        return NW_OK;
+    }
+    p->wtab_valid = true;
+    return NW_OK;
+}
+
 int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
-    const bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
+    bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
     // rocFFT may use its input as scratch: transform from the plan's own copy.
     if (xs_dev != p->d_x)
         NW_TRY(staged(p, ST_COPY, [&] {
@@ -323,15 +345,14 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
     }
     if (!rocfft_engine && p->chirp) {
         // chirp-z form (any other n up to 8192 fp32 / 4096 fp64): two on-chip FFTs per row
-        if (!p->wtab_valid) {
-            NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes, nw::chirp_wtable_bytes(p->n, p->nfreq, p->dtype, p->desc.kind)));
-            NW_HIP(nw::build_chirp_wtable(p->desc, p->dtype, p->d_wtab, p->stream, p->chirp_counts));
-            p->wtab_valid = true;
-        }
-        return staged(p, ST_FUSED, [&] {
-            NW_HIP(nw::launch_chirp(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->chirp_counts, p->stream));
-            return NW_OK;
-        });
+        NW_TRY(chirp_table(p));
+        if (p->chirp)
+            return staged(p, ST_FUSED, [&] {
+                NW_HIP(nw::launch_chirp(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->chirp_counts,
+                                        p->stream));
+                return NW_OK;
+            });
+        rocfft_engine = true;   // a tentative length whose rows do not fit: the rocFFT engine
     }
     if (!rocfft_engine) {
         if (!p->wtab_valid) {
@@ -626,8 +647,12 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     p->flags = flags;
     p->esz = dtype == NW_F32 ? 4 : 8;
     const bool large_ok = !nw::fused_supported(n, dtype) && nw::large_supported(n, dtype);
-    const bool chirp_ok = nw::chirp_supported(n, dtype) && !(flags & NW_NO_CHIRP);
-    const bool fused_ok = nw::fused_supported(n, dtype) || large_ok || chirp_ok;
+    const bool chirp_sure = nw::chirp_supported(n, dtype) && !(flags & NW_NO_CHIRP);
+    // 2n - 1 > M_max: the chirp-z form only if the auto engine finds every row narrow enough
+    const bool chirp_maybe = !chirp_sure && !large_ok && nw::chirp_possible(n, dtype) && !(flags & NW_NO_CHIRP) &&
+                             !(flags & (NW_ENGINE_ROCFFT | NW_ENGINE_FUSED));
+    const bool chirp_ok = chirp_sure || chirp_maybe;
+    const bool fused_ok = nw::fused_supported(n, dtype) || large_ok || chirp_sure;
     if (flags & NW_ENGINE_FUSED) {
         if (!fused_ok) {
             free_plan(p);
@@ -637,10 +662,11 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
     } else if (flags & NW_ENGINE_ROCFFT) {
         p->engine = NW_ENGINE_ROCFFT;
     } else {
-        p->engine = fused_ok ? NW_ENGINE_FUSED : NW_ENGINE_ROCFFT;
+        p->engine = (fused_ok || chirp_maybe) ? NW_ENGINE_FUSED : NW_ENGINE_ROCFFT;
     }
     p->large = p->engine == NW_ENGINE_FUSED && large_ok;
     p->chirp = p->engine == NW_ENGINE_FUSED && chirp_ok;
+    p->chirp_tentative = p->chirp && chirp_maybe;
     p->stats.engine = p->engine;
     auto bail = [&](int code) {
         free_plan(p);
@@ -980,6 +1006,11 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
     p->desc = d;
     p->has_wavelet = true;
     p->wtab_valid = false;
+    if (p->chirp_tentative) {   // a new wavelet may fit where the last one did not
+        p->chirp = true;
+        p->engine = NW_ENGINE_FUSED;
+        p->stats.engine = NW_ENGINE_FUSED;
+    }
     return setup_unique_rows(p, kind, freqs, peak, xstep, normal ? nullptr : table);
 }
 
@@ -1025,6 +1056,14 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     d.scale = 1.0 / (double)p->n;
     d.off = d.len_full < p->n ? (p->n - d.len_full) / 2 : 0;
     d.xlim = (p->flags & NW_INTERPOLATE) ? p->n / 2 : p->n;   // int(n / 2) (base.py:120)
+    if (p->chirp && p->chirp_tentative && !p->wtab_valid) {   // settle the engine before any buffer choice
+        if (p->dedup) {
+            UniqueRows u(p);
+            NW_TRY(chirp_table(p));
+        } else {
+            NW_TRY(chirp_table(p));
+        }
+    }
 
     if (is_reduction(out_kind)) return execute_reduce(p, x, nsig, out, out_kind, mem == NW_MEM_HOST);
 

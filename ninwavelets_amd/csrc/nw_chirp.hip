@@ -340,10 +340,17 @@ hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wta
     X(float, 8192, NW_CHIRP_E) X(float, 16384, 32)                                               \
     X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) X(double, 8192, 16)
 
+int64_t chirp_mmax(int dtype) { return dtype == NW_F32 ? 16384 : 8192; }
+
 bool chirp_supported(int64_t n, int dtype) {
     if (n < 1 || fused_supported(n, dtype)) return false;
-    const int64_t mmax = dtype == NW_F32 ? 16384 : 8192;
-    return (dtype == NW_F32 || dtype == NW_F64) && 2 * n - 1 <= mmax;
+    return (dtype == NW_F32 || dtype == NW_F64) && 2 * n - 1 <= chirp_mmax(dtype);
+}
+
+// longer lengths (up to M_max - 1) fit when every row's support does (M >= n + K - 1)
+bool chirp_possible(int64_t n, int dtype) {
+    if (n < 1 || fused_supported(n, dtype) || (dtype != NW_F32 && dtype != NW_F64)) return false;
+    return n < chirp_mmax(dtype);
 }
 
 // table buffer: W rows, then ksup[nfreq], then the row map (rows grouped by M class)
@@ -355,7 +362,7 @@ size_t chirp_wtable_bytes(int64_t n, int nfreq, int dtype, int kind) {
     return chirp_w_bytes(n, nfreq, dtype, kind) + 2 * (size_t)nfreq * sizeof(int);
 }
 
-hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts) {
+hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts, bool* fits) {
     dim3 grid((unsigned)((d.n + 255) / 256), (unsigned)d.nfreq);
     const bool realw = d.kind != NW_TABLE;
     int* ksup = reinterpret_cast<int*>(reinterpret_cast<char*>(wtab) + chirp_w_bytes(d.n, d.nfreq, dtype, d.kind));
@@ -378,11 +385,13 @@ hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t
     if (e == hipSuccess) e = hipMemcpyAsync(ks.data(), ksup, d.nfreq * sizeof(int), hipMemcpyDeviceToHost, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     if (e != hipSuccess) return e;
-    const int64_t mfull = chirp_m(d.n);
+    const int64_t mfull = std::min<int64_t>(chirp_m(d.n), chirp_mmax(dtype));
     std::vector<int> cls(d.nfreq);
     for (int c = 0; c < kChirpClasses; ++c) counts[c] = 0;
+    *fits = true;
     for (int f = 0; f < d.nfreq; ++f) {
         const int64_t need = std::max<int64_t>(d.n + std::max(ks[f], 1) - 1, 2 * (int64_t)ks[f]);
+        if (need > mfull) *fits = false;
         int64_t m = 1024;
         while (m < need && m < mfull) m <<= 1;
         int c = 0;
@@ -401,7 +410,7 @@ hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t
 
 hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
                         int64_t nsig, const int64_t* counts, hipStream_t s) {
-    if (!chirp_supported(d.n, dtype)) return hipErrorNotSupported;
+    if (!chirp_possible(d.n, dtype)) return hipErrorNotSupported;
     const bool realw = d.kind != NW_TABLE;
     const int* rowmap = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
                                                      chirp_w_bytes(d.n, d.nfreq, dtype, d.kind)) + d.nfreq;

@@ -178,10 +178,11 @@ hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 p
 // chirp-z engine (nw_chirp.hip): n not taken by the power-of-two kernels, 2n - 1 <= 16384
 // (fp32) / 8192 (fp64); one (scale, signal) row = two on-chip FFTs of M = 2^ceil(log2(2n-1))
 bool       chirp_supported(int64_t n, int dtype);
+bool       chirp_possible(int64_t n, int dtype);   // also n < M_max when every row's support fits
 size_t     chirp_wtable_bytes(int64_t n, int nfreq, int dtype, int kind);
 // builds W, each row's support and the rows grouped by M class (M = 1024 << c, c < 5:
 // counts[c] rows each; synchronises s once); launch_chirp runs one kernel per class
-hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts);
+hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts, bool* fits);
 hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
                         int64_t nsig, const int64_t* counts, hipStream_t s);
 

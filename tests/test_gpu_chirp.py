@@ -133,3 +133,27 @@ def test_chirp_rows_of_different_transform_sizes(dtype):
     got = q.execute(x, out_kind='cwt')
     ref = np.stack([O.cwt_from_rows(xi.astype(np.float64), list(tab), False) for xi in x])
     assert within(got, ref, dtype, 'cwt')
+
+
+@pytest.mark.parametrize('dtype,n', [('float32', 10001), ('float32', 14001), ('float64', 5001)])
+def test_chirp_tentative_lengths(dtype, n):
+    """2n - 1 beyond the largest on-chip transform: the auto engine takes the chirp-z form
+    when every row's support K fits (n + K - 1 <= 16384 fp32 / 8192 fp64), and falls back
+    to the rocFFT engine for a wavelet with a wide row -- re-armed by the next wavelet."""
+    S = 2
+    x = synth(S, n, 55).astype(dtype)
+    narrow = np.array([2., 5., 11.])
+    p = chirp_plan(n, 3, dtype, 'morse', (17.5, 3.), narrow, max_batch=2)
+    got = p.execute(x, out_kind='cwt')
+    assert p.stats()['engine'] == 'fused'
+    assert within(got, oracle('morse', x, narrow, 'cwt'), dtype, 'cwt')
+    wide = np.array([2., 5., 400.])                  # 400 Hz: support ~ n
+    g = L.trans_grid(n / 1000., 1000., False)
+    p.set_wavelet('morse', [17.5, 3.], wide, g)
+    got = p.execute(x, out_kind='power')
+    assert p.stats()['engine'] == 'rocfft'
+    assert within(got, oracle('morse', x, wide, 'power'), dtype, 'power')
+    p.set_wavelet('morse', [17.5, 3.], narrow, g)
+    got = p.execute(x, out_kind='abs')
+    assert p.stats()['engine'] == 'fused'
+    assert within(got, oracle('morse', x, narrow, 'abs'), dtype, 'abs')
