@@ -818,8 +818,12 @@ static int setup_unique_rows(nw_plan* p, int kind, const double* freqs, const st
         for (int f = 0; f < F; ++f) {
             const int64_t len = p->row_len_host.empty() ? L : p->row_len_host[f];
             const unsigned char* b = (const unsigned char*)(t + (size_t)f * L * 2);
-            uint64_t h = 1469598103934665603ull ^ (uint64_t)len;
-            for (size_t i = 0; i < (size_t)len * 16; ++i) h = (h ^ b[i]) * 1099511628211ull;
+            uint64_t h = 1469598103934665603ull ^ (uint64_t)len;   // FNV-1a over 8-byte words
+            for (size_t i = 0; i < (size_t)len * 2; ++i) {
+                uint64_t w;
+                std::memcpy(&w, b + 8 * i, 8);
+                h = (h ^ w) * 1099511628211ull;
+            }
             int found = -1;
             for (int g : seen[h]) {
                 const int64_t lg = p->row_len_host.empty() ? L : p->row_len_host[g];
