@@ -51,6 +51,9 @@ __device__ __forceinline__ C2<float> hi(C2<f2> p) { return {p.re.y, p.im.y}; }
 #ifndef NW_PK
 #define NW_PK 1   // packed fp32 math for pairs of butterflies (Q >= 2 passes)
 #endif
+#ifndef NW_TW_PAIR
+#define NW_TW_PAIR 1   // paired last pass: second butterfly's twiddle bases from the first's
+#endif
 
 template <typename T> __device__ __forceinline__ C2<T> cmul(C2<T> a, C2<T> b) {
     return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
@@ -644,7 +647,13 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
         constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;
         C2<S> pb[Q][LR > 0 ? LR : 1];
 #ifndef NW_ABL_NOTWIDDLE
-        if constexpr (!TABLED) {
+        if constexpr (!TABLED && I::PAIRED && Q == 2 && NW_TW_PAIR) {
+            // the lane's second butterfly is j + 1 (j even, no wrap mod NS): its bases are the
+            // first's times the constants w^(2^k) -- uniform loads from the exact table
+            twiddle_bases<S, R, N, I::NS * R>(pb[0], I::bfly(t, 0) % I::NS, tw);
+#pragma unroll
+            for (int k = 0; k < LR; ++k) pb[1][k] = cmul(pb[0][k], tw[(N / (I::NS * R)) << k]);
+        } else if constexpr (!TABLED) {
 #pragma unroll
             for (int q = 0; q < Q; ++q) twiddle_bases<S, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
         }
