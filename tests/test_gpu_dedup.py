@@ -42,7 +42,8 @@ def plan_pair(n, F, dtype, kind, params, freqs, engine, max_batch=4, interpolate
 
 
 # (n, engine): rocFFT engine (odd n too), the one-pass fused kernel, the two-pass form
-CASES = [(1000, 'rocfft'), (301, 'rocfft'), (4096, 'fused'), (16384, 'fused'), (1 << 15, 'fused')]
+CASES = [(1000, 'rocfft'), (301, 'rocfft'), (1000, None), (301, None), (4096, 'fused'), (16384, 'fused'),
+         (1 << 15, 'fused')]   # None: the auto engine, i.e. the chirp-z form at 1000 and 301
 
 
 @pytest.mark.parametrize('n,engine', CASES)

@@ -35,7 +35,7 @@ def plans_for(n, freqs, dtype, engine, kind, params, world, max_batch=2):
     return out
 
 
-@pytest.mark.parametrize('n,engine', [(1000, 'rocfft'), (4096, None), (1 << 15, None)])
+@pytest.mark.parametrize('n,engine', [(1000, 'rocfft'), (1000, None), (4096, None), (1 << 15, None)])
 @pytest.mark.parametrize('dtype', ['float32', 'float64'])
 @pytest.mark.parametrize('world', [2, 3])
 def test_scale_slices_equal_single_plan(n, engine, dtype, world):
