@@ -98,7 +98,7 @@ template <typename T, int M, int E, int OUT, bool REALW>
 __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     WDesc d, const cplx<T>* __restrict__ X, const void* __restrict__ wtab, void* __restrict__ out,
     const C2<T>* __restrict__ tw, const C2<T>* __restrict__ bh, const C2<T>* __restrict__ ct, int64_t nsig,
-    int nsg_pad, const int* __restrict__ rowmap, int nrows) {
+    int nsg_pad, const int* __restrict__ rowmap, int nrows, const int* __restrict__ ksup) {
     using G = Geometry<M, E>;
     constexpr int TT = G::T;
     constexpr int LP = G::npass() - 1;
@@ -127,22 +127,31 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     const uint32_t n2 = 2u * (uint32_t)n;
     const float inv_n2 = 1.0f / (float)n2;
     const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * n;
+    const int nz = (ksup[fi] + TT - 1) / TT;   // pass-0 elements reaching the support (<= E/2)
     Tab1<T, M, E>::fill(lds, tw, t);
     for (int64_t s = s_begin; s < s_end; ++s) {
         const cplx<T>* Xs = X + s * d.nh;
         C2<T> v[E];
         // a[k] = W X c(k), conjugated: the forward FFT through the inverse passes
+        // only the elements r < NZ (bins k < NZ*T) can meet the row's support K <= M/2: the
+        // others are zero for every thread and the DIF stages skip them (as nw_fused's pass 0)
+        auto pass0 = [&]<int NZ>() {
 #pragma unroll
-        for (int r = 0; r < E; ++r) {
-            const int k = t + r * TT;
-            C2<T> a{T(0), T(0)};
-            if (k < n) {
-                const C2<T> z = WRow<T, REALW>::apply(wrow[k], spectrum_bin<T>(Xs, d, k));
-                a = cmul(z, chirp<T>(k, n2, inv_n2, ct));
+            for (int r = 0; r < E; ++r) {
+                const int k = t + r * TT;
+                C2<T> a{T(0), T(0)};
+                if (r < NZ && k < n) {
+                    const C2<T> z = WRow<T, REALW>::apply(wrow[k], spectrum_bin<T>(Xs, d, k));
+                    a = cmul(z, chirp<T>(k, n2, inv_n2, ct));
+                }
+                v[r] = C2<T>{a.re, -a.im};
             }
-            v[r] = C2<T>{a.re, -a.im};
-        }
-        idft_br<T, E, E / 2>(v);   // n <= M/2: elements r >= E/2 (k >= M/2) are zero
+            idft_br<T, E, NZ>(v);
+        };
+        if (nz <= 1) pass0.template operator()<1>();
+        else if (nz <= 2) pass0.template operator()<2>();
+        else if (nz <= 4) pass0.template operator()<4>();
+        else pass0.template operator()<E / 2>();
         passes_regs<T, M, E, 1>(v, lds, t, tw);
         // P[m] = conj(v[m]) * Bh[m]
 #pragma unroll
@@ -299,7 +308,7 @@ hipError_t chirp_tables(int64_t n, int64_t m, int dtype, void** out) {
 
 template <typename T, int M, int E, bool REALW>
 hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
-                    const int* rowmap, int nrows, hipStream_t s) {
+                    const int* rowmap, int nrows, const int* ksup, hipStream_t s) {
     constexpr int threads = M / E;
     const int lds = kLdsBytes<T, M, E>;
     void* tw = nullptr;
@@ -320,7 +329,8 @@ hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wta
     auto go = [&](auto kern) {
         e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return;
-        kern<<<(unsigned)blocks, threads, lds, s>>>(d, Xc, wtab, out, twc, bh, ct, nsig, (int)nsg_pad, rowmap, nrows);
+        kern<<<(unsigned)blocks, threads, lds, s>>>(d, Xc, wtab, out, twc, bh, ct, nsig, (int)nsg_pad, rowmap, nrows,
+                                                    ksup);
         e = hipGetLastError();
     };
     if (out_kind == NW_OUT_CWT) go(nw_chirp_kernel<T, M, E, NW_OUT_CWT, REALW>);
@@ -412,8 +422,9 @@ hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, 
                         int64_t nsig, const int64_t* counts, hipStream_t s) {
     if (!chirp_possible(d.n, dtype)) return hipErrorNotSupported;
     const bool realw = d.kind != NW_TABLE;
-    const int* rowmap = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
-                                                     chirp_w_bytes(d.n, d.nfreq, dtype, d.kind)) + d.nfreq;
+    const int* ksup = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
+                                                   chirp_w_bytes(d.n, d.nfreq, dtype, d.kind));
+    const int* rowmap = ksup + d.nfreq;
     int64_t off = 0;
     for (int c = 0; c < kChirpClasses; ++c) {
         const int64_t cnt = counts[c];
@@ -422,8 +433,8 @@ hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, 
         hipError_t e = hipErrorNotSupported;
 #define NW_CHIRP_LAUNCH(TY, MM, EE)                                                                             \
         if (m == MM && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64))                                            \
-            e = realw ? launch_m<TY, MM, EE, true>(d, out_kind, X, wtab, out, nsig, rowmap + off, (int)cnt, s) \
-                      : launch_m<TY, MM, EE, false>(d, out_kind, X, wtab, out, nsig, rowmap + off, (int)cnt, s);
+            e = realw ? launch_m<TY, MM, EE, true>(d, out_kind, X, wtab, out, nsig, rowmap + off, (int)cnt, ksup, s) \
+                      : launch_m<TY, MM, EE, false>(d, out_kind, X, wtab, out, nsig, rowmap + off, (int)cnt, ksup, s);
         NW_CHIRP_TABLE(NW_CHIRP_LAUNCH)
 #undef NW_CHIRP_LAUNCH
         if (e != hipSuccess) return e;
