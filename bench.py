@@ -64,7 +64,7 @@ def synth_device(torch, S, n, seed, device, sfreq=1000., dtype=None):
     return x
 
 
-def pmc_traffic(kernel, config, chunk, engine, dtype='float32', out=None):
+def pmc_traffic(kernel, config, chunk, engine, dtype='float32', out=None, n=None):
     """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
     same bench command (tools/gpu_round.sh -> profiles/pmc_<config>_<engine>.json, or
     profiles/pmc_<config>_<kernel>.json for a second kernel of one config), or None
@@ -84,6 +84,8 @@ def pmc_traffic(kernel, config, chunk, engine, dtype='float32', out=None):
     if d.get('kernel') != kernel or c.get('chunk') != chunk or c.get('dtype', 'float32') != dtype:
         return None
     if out is not None and c.get('out', out) != out:
+        return None
+    if n is not None and c.get('n', n) != n:
         return None
     return d.get('hbm_bytes_per_launch')
 
@@ -311,7 +313,7 @@ def main():
         roof = {'kernel': kname, 'bound': 'hbm',
                 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
                 'frac': round(achieved / PEAK_HBM_GBPS, 4),
-                'traffic': pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind),
+                'traffic': pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind, n),
                 'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
         stage_ms = {k: round(st[k] / args.steps, 3) for k in
                     ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_rows', 'ms_expand',
