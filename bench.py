@@ -10,13 +10,22 @@ complex output (1.1 TB per GPU per step) is streamed through two rotating HBM
 chunk buffers.  Signals are sharded over ranks with no collective on the data
 path (the barrier and a max-reduce of the elapsed time are timing only).
 
-    python bench.py [--gpus N --steps K --warmup W] [--config c4|c3|c2] [--engine auto|rocfft|fused]
+    python bench.py [--gpus N --steps K --warmup W] [--config c4|c3|c2|c5] [--engine auto|rocfft|fused]
+
+Multi-GPU: under torchrun (WORLD_SIZE set) every process is one rank.  Without it,
+``--gpus N`` (N > 1) makes this process a launcher that never touches the GPU: it starts
+N fresh child processes (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+MASTER_PORT), waits for them and prints rank 0's line.  ``--dry-run --backend gloo``
+runs the same multi-rank flow on CPU without any kernel (tests/test_bench_cpu.py).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -64,30 +73,40 @@ def synth_device(torch, S, n, seed, device, sfreq=1000., dtype=None):
     return x
 
 
+def source_hash() -> str:
+    """sha256 (16 hex) over the engine's sources (csrc/*.hip, *.h, *.cpp, include/ninwave.h):
+    a PMC summary is attached to a bench line only when it was collected on these sources."""
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, 'ninwavelets_amd', 'csrc')
+    files = sorted(f for f in os.listdir(csrc) if f.endswith(('.hip', '.h', '.cpp')))
+    for f in files + ['../../include/ninwave.h']:
+        with open(os.path.join(csrc, f), 'rb') as fh:
+            h.update(os.path.basename(f).encode() + b'\0' + fh.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(kernel, config, chunk, engine, dtype='float32', out=None, n=None):
-    """HBM bytes per launch of `kernel` from the committed rocprofv3 PMC summary of this
-    same bench command (tools/gpu_round.sh -> profiles/pmc_<config>_<engine>.json, or
-    profiles/pmc_<config>_<kernel>.json for a second kernel of one config), or None
-    when the summary was taken on another kernel, chunk, dtype or output kind."""
-    d = None
-    for name in (f'pmc_{config}_{engine}.json', f'pmc_{config}_{kernel}.json'):
+    """(HBM bytes per launch, source) of `kernel` from the committed rocprofv3 PMC summary
+    of this same bench command (tools/prof_counters.sh -> profiles/pmc_<config>_*.json):
+    None unless the summary was taken on this kernel, chunk, dtype, output kind, n AND on
+    the current engine sources (source_hash), so a stale profile is never reported."""
+    import glob
+    want = source_hash()
+    for path in sorted(glob.glob(os.path.join(ROOT, 'profiles', f'pmc_{config}_*.json'))):
         try:
-            with open(os.path.join(ROOT, 'profiles', name)) as f:
+            with open(path) as f:
                 d = json.load(f)
         except (OSError, ValueError):
             continue
-        if d.get('kernel') == kernel:
-            break
-    if d is None:
-        return None
-    c = d.get('config', {})
-    if d.get('kernel') != kernel or c.get('chunk') != chunk or c.get('dtype', 'float32') != dtype:
-        return None
-    if out is not None and c.get('out', out) != out:
-        return None
-    if n is not None and c.get('n', n) != n:
-        return None
-    return d.get('hbm_bytes_per_launch')
+        c = d.get('config', {})
+        if d.get('kernel') != kernel or c.get('chunk') != chunk or c.get('dtype', 'float32') != dtype:
+            continue
+        if (out is not None and c.get('out', out) != out) or (n is not None and c.get('n', n) != n):
+            continue
+        if c.get('src_hash') != want:
+            continue
+        return d.get('hbm_bytes_per_launch'), os.path.relpath(path, ROOT)
+    return None, None
 
 
 def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0):
@@ -118,7 +137,7 @@ def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0):
             if el >= budget_s:
                 break
     return {'value': rows_done * n / el, 'unit': 'points/s', 'cores': 1, 'kind': 'port',
-            'sample_seconds': el, 'rows_done': rows_done,
+            'cpu_model': cpu_model(), 'sample_seconds': el, 'rows_done': rows_done,
             'sample': f'{rows_done} (signal, freq) rows of {n} samples over {sigs} signal(s) '
                       f'({kind} {out_kind}, oracle/nw_oracle.py single process, wavelet rows '
                       f'cached), {el:.1f} s'}
@@ -131,21 +150,70 @@ def _pool_worker(args):
     return r['value'] * r['sample_seconds'], r['sample_seconds'], r['rows_done']
 
 
-def cpu_baseline_pool(kind, n, freqs, out_kind, budget_s=8.0, workers=16):
-    """The same oracle work in a multiprocessing Pool over signals (BASELINE.md §3 mode b):
-    each worker times its own bounded sample; the rate is the sum of the workers' rates."""
+def cpu_model() -> str:
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def cpu_baseline_pool(kind, n, freqs, out_kind, budget_s=8.0, workers=None):
+    """The same oracle work in multiprocessing.Pool(os.cpu_count()) over signals
+    (BASELINE.md §3 mode b, uncapped): each worker times its own bounded sample; the rate
+    is the sum of the workers' rates.  cores = the pool size; the CPUs this process may
+    run on (sched_getaffinity) and the CPU model are recorded beside it."""
     import multiprocessing as mp
-    workers = max(1, min(workers, os.cpu_count() or 1))
+    workers = workers or os.cpu_count() or 1
     with mp.get_context('spawn').Pool(workers) as pool:
         res = pool.map(_pool_worker, [(kind, n, list(freqs), out_kind, budget_s, i) for i in range(workers)])
     rate = sum(pts / el for pts, el, _ in res)
     rows = sum(r for _, _, r in res)
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = None
     return {'value': rate, 'unit': 'points/s', 'cores': workers, 'kind': 'port',
+            'cpu_model': cpu_model(), 'os_cpu_count': os.cpu_count(), 'cpus_allowed': allowed,
             'sample': f'{rows} (signal, freq) rows of {n} samples over {workers} processes '
-                      f'(multiprocessing Pool, each ~{budget_s:.0f} s; sum of per-process rates)'}
+                      f'(multiprocessing.Pool(os.cpu_count()), each ~{budget_s:.0f} s; sum of '
+                      f'per-process rates)'}
 
 
-def main():
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(nranks: int, argv) -> int:
+    """Parent of an N-rank run started without torchrun: it never touches the GPU (no
+    torch import), starts one fresh child per rank, forwards rank 0's stdout and returns
+    the first non-zero exit status (children are never exec'd from a GPU process)."""
+    port = free_port()
+    procs = []
+    for r in range(nranks):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nranks),
+                   LOCAL_WORLD_SIZE=str(nranks), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
+    out0 = procs[0].stdout.read().decode()
+    rcs = [p.wait() for p in procs]
+    for ln in out0.splitlines():              # the JSON line to stdout, library chatter to stderr
+        (sys.stdout if ln.startswith('{') else sys.stderr).write(ln + '\n')
+    sys.stdout.flush()
+    bad = [rc for rc in rcs if rc != 0]
+    if bad:
+        log(f'[bench] rank exit codes: {rcs}')
+    return bad[0] if bad else 0
+
+
+def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
@@ -169,19 +237,39 @@ def main():
                          'or the scale list of the same signals (strong scaling; the C5 split for '
                          'one long signal, SURVEY §8e)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    args = ap.parse_args()
+    ap.add_argument('--backend', default=None, choices=['nccl', 'gloo'],
+                    help='process-group backend for N > 1 ranks (default: nccl = RCCL over xGMI; '
+                         'gloo with --dry-run)')
+    ap.add_argument('--dry-run', action='store_true',
+                    help='no GPU and no kernels: exercise the launcher, the process group, the '
+                         'barriers and the max-over-ranks timing on CPU (tests)')
+    args = ap.parse_args(argv)
+
+    if 'WORLD_SIZE' in os.environ:           # torchrun or our own launcher: this process is a rank
+        world = int(os.environ['WORLD_SIZE'])
+        if args.gpus != 1 and args.gpus != world:
+            raise SystemExit(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={world}')
+    elif args.gpus > 1:                      # launcher: N fresh ranks, no GPU call here
+        return launch_ranks(args.gpus, sys.argv[1:] if argv is None else argv)
+    else:
+        world = 1
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    backend = args.backend or ('gloo' if args.dry_run else 'nccl')
 
     import torch
     import torch.distributed as dist
+    if args.dry_run:
+        return dry_run(args, torch, dist, world, rank, backend)
     import ninwavelets_amd as nw
     from ninwavelets_amd import _lib as L
 
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
@@ -247,10 +335,7 @@ def main():
         step()
     barrier()
     el = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = max_over_ranks(torch, dist, el, world, dev if backend == 'nccl' else None)
     st = plan.stats()
     points = float(S) * F_all * n * args.steps * (1 if by_scales else world)
     value = points / el
@@ -299,8 +384,7 @@ def main():
                 'avg_launch_ms': round(rows_ms, 4), 'algorithmic_bytes_per_launch': rows_bytes}
         else:
             per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
-            chirp = fused and (n < 1024 or n & (n - 1))      # nw_chirp.hip: two on-chip FFTs per row
-            kname = ('nw_chirp_kernel' if chirp else 'nw_fused') if fused else 'k1_multiply'
+            kname = L.KERNEL_NAMES[st['kernel']]          # the kernel rocprofv3 shows for this launch
         if two_pass or kname == 'k_expand_rows':
             # end to end against the path's minimum traffic (X read once, every output once)
             oe = (2 if out_kind == 'cwt' else 1) * esz
@@ -310,10 +394,14 @@ def main():
                 'achieved': round(min_bytes / (el / args.steps) / 1e9, 1), 'unit': 'GB/s',
                 'frac': round(min_bytes / (el / args.steps) / 1e9 / PEAK_HBM_GBPS, 4)}
         achieved = per_launch / (ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind, n)
         roof = {'kernel': kname, 'bound': 'hbm',
                 'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
                 'frac': round(achieved / PEAK_HBM_GBPS, 4),
-                'traffic': pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind, n),
+                'traffic': traffic,
+                'traffic_source': (f'{traffic_src}: rocprofv3 PMC passes of this command, 2*FETCH_SIZE + '
+                                   f'WRITE_SIZE per launch, on engine sources {source_hash()}'
+                                   if traffic_src else 'no PMC summary on the current engine sources'),
                 'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
         stage_ms = {k: round(st[k] / args.steps, 3) for k in
                     ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_rows', 'ms_expand',
@@ -343,7 +431,54 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def max_over_ranks(torch, dist, el, world, device):
+    """The step time the job took: the MAX of every rank's elapsed time."""
+    if world <= 1:
+        return el
+    t = torch.tensor([el], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def dry_run(args, torch, dist, world, rank, backend):
+    """The multi-rank flow without a GPU: process group, warmup, barrier-bracketed timed
+    steps (a fixed CPU stand-in per step), MAX over ranks, rank 0's line.  Its value is
+    not a measurement; it proves the launcher and the rank plumbing (tests)."""
+    if world > 1:
+        dist.init_process_group(backend)
+    kind, epochs, chans, n, freqs, out_kind, dtype, text = CONFIGS[args.config]
+
+    def step():
+        time.sleep(0.01 * (1 + rank))        # ranks of unequal speed: the max must win
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        step()
+        barrier()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    el = max_over_ranks(torch, dist, time.perf_counter() - t0, world, None)
+    if rank == 0:
+        print(json.dumps({
+            'metric': 'CWT throughput (epochs*chans*samples*freqs)/s', 'value': None, 'unit': 'points/s',
+            'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': el / max(1, args.steps) * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'vs_baseline': None, 'dtype': 'f64' if dtype == 'float64' else 'f32',
+            'data': 'dry run: no GPU, no kernels', 'backend': backend,
+            'config': {'workload': text, 'parallelism': f'dp{world}'}}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main())

@@ -118,7 +118,16 @@ typedef struct nw_stats {
     double  ms_expand;      /* repeated rows: copies of the computed unique rows */
     int64_t launches_expand;
     int64_t unique_rows;    /* scale rows actually computed (nfreq unless rows repeat) */
+    int64_t kernel;         /* NW_K_*: the output-writing kernel of the last chunk */
 } nw_stats;
+
+/* nw_stats.kernel: which kernel wrote the output rows (the dominant kernel of a step) */
+#define NW_K_NONE        0
+#define NW_K_FUSED       1   /* nw_fused_kernel (one pass, one signal per lane value)        */
+#define NW_K_FUSED_PAIR  2   /* nw_fused_pair_kernel (one pass, two signals per lane value)  */
+#define NW_K_CHIRP       3   /* nw_chirp_kernel (chirp-z form)                               */
+#define NW_K_TWO_PASS    4   /* rows_kernel + cols_kernel (n > 16384; cols writes the output) */
+#define NW_K_MULTIPLY    5   /* k1_multiply + rocFFT inverse (+ k2_epilogue): rocFFT engine   */
 
 typedef struct nw_plan nw_plan;
 
@@ -173,12 +182,25 @@ int nw_plan_wavelet_rows(nw_plan* plan, void* out_host);
  * asynchronous on the plan stream (see nw_plan_sync). */
 int nw_execute(nw_plan* plan, const void* x, int64_t nsig, void* out, int out_kind, int mem);
 
-/* Shard nsig host signals over ndev plans (one per device, identical config),
- * one host thread per device; contiguous blocks of signals per device.  For the
- * reduction kinds each device sums its block and the host adds the fp64 partial
- * sums in device order before the mean / |.| of the result. */
+/* Shard nsig host signals over nplans plans (one per device, identical config),
+ * one host thread per plan; balanced contiguous blocks (nsig / nplans signals, one
+ * more for the first nsig % nplans plans).  A plan is not reentrant, so a plan
+ * pointer may appear only once (NW_E_INVALID otherwise; two plans on one device are
+ * fine).  For the reduction kinds each device sums its block and the host adds the
+ * fp64 partial sums in device order before the mean / |.| of the result.
+ * Replaces the serial per-epoch loop of EpochsWavelet.cwt (mneutils.py:39). */
 int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t nsig,
                      void* out, int out_kind);
+
+/* Device-resident sharding (one process, one host thread per device, no
+ * PCIe): plan i transforms nsig[i] signals x[i] -- a DEVICE pointer on plan i's
+ * device -- into out[i] (device pointer, same device, (nsig[i], F, n)).  Returns when
+ * every device has finished.  Reduction kinds: each device sums its block in fp64,
+ * device 0 gathers the partial sums peer-to-peer, adds them in device order and
+ * writes the (F, n) result to out[0] (out[i > 0] unused).  Plans must be distinct and
+ * share n, nfreq and dtype. */
+int nw_execute_multi_device(nw_plan* const* plans, int nplans, const void* const* x,
+                            const int64_t* nsig, void* const* out, int out_kind);
 
 /* Shard the SCALES instead (one long signal, e.g. C5, cannot shard by
  * signal): plan i (its own device, same n / dtype / flags) holds the i-th contiguous
@@ -227,6 +249,9 @@ int nw_make_wavelets(int device, int kind, const double* params, int nparams, co
                      double sfreq, double real_wave_length, void* out, int64_t* max_len, int64_t* row_len);
 
 int nw_plan_set_stream(nw_plan* plan, void* hip_stream);   /* NULL: the plan's own stream */
+/* The hipStream_t the plan currently launches on (for event ordering with the caller's
+ * streams: device-buffer executes are asynchronous on it). */
+int nw_plan_get_stream(nw_plan* plan, void** hip_stream);
 int nw_plan_sync(nw_plan* plan);
 int nw_plan_stats(nw_plan* plan, nw_stats* stats);
 int nw_plan_reset_stats(nw_plan* plan);

@@ -5,16 +5,17 @@
 
 Exports the reference's hot-path API (ninwavelets/__init__.py:1-3):
 WaveletBase, WaveletMode, Morse, MorseMNE, Morlet, Haar, MexicanHat, Shannon,
-EpochsWavelet; plus the batched device engine (``Plan``).  Plotting and
-``Baseline`` are outside the accelerated path and not provided.
+EpochsWavelet, Baseline; plus the batched device engine (``Plan``,
+``execute_multi``, ``execute_multi_device``).  Plotting is outside the accelerated
+path and not provided.
 """
 from .base import WaveletBase, WaveletMode, pad_to, interpolate_alias
 from .wavelets import Morse, MorseMNE, Morlet, Haar, MexicanHat, Shannon
 from .mneutils import EpochsWavelet
 from .baseline import Baseline, baseline_of
-from .engine import Plan, execute_multi
+from .engine import Plan, execute_multi, execute_multi_device
 from . import _lib
 
 __all__ = ['Baseline', 'baseline_of', 'WaveletBase', 'WaveletMode', 'Morse', 'MorseMNE', 'Morlet', 'Haar', 'MexicanHat',
-           'Shannon', 'EpochsWavelet', 'Plan', 'execute_multi', 'pad_to', 'interpolate_alias']
+           'Shannon', 'EpochsWavelet', 'Plan', 'execute_multi', 'execute_multi_device', 'pad_to', 'interpolate_alias']
 __version__ = '0.1.0'

@@ -37,6 +37,9 @@ NW_NO_CHIRP = 0x400
 NW_OUT_CWT, NW_OUT_ABS, NW_OUT_POWER = 0, 1, 2
 NW_OUT_POWER_MEAN, NW_OUT_ITC, NW_OUT_POWER_SUM, NW_OUT_PHASE_SUM = 3, 4, 5, 6
 NW_MEM_HOST, NW_MEM_DEVICE = 0, 1
+# nw_stats.kernel -> the kernel name rocprofv3 shows
+KERNEL_NAMES = {0: None, 1: 'nw_fused_kernel', 2: 'nw_fused_pair_kernel', 3: 'nw_chirp_kernel',
+                4: 'cols_kernel', 5: 'k1_multiply'}
 NW_BL = {'mean': 0, 'ratio': 1, 'percent': 2, 'log': 3, 'zscore': 4, 'zlog': 5}
 
 
@@ -52,7 +55,8 @@ class nw_stats(ctypes.Structure):
                 ('launches_multiply', ctypes.c_int64), ('launches_fused', ctypes.c_int64),
                 ('engine', ctypes.c_int64), ('ms_rows', ctypes.c_double),
                 ('launches_rows', ctypes.c_int64), ('ms_expand', ctypes.c_double),
-                ('launches_expand', ctypes.c_int64), ('unique_rows', ctypes.c_int64)]
+                ('launches_expand', ctypes.c_int64), ('unique_rows', ctypes.c_int64),
+                ('kernel', ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}
@@ -77,6 +81,8 @@ SIGNATURES = [
     ('nw_execute', ctypes.c_int, [_P, _P, _I64, _P, ctypes.c_int, ctypes.c_int]),
     ('nw_execute_multi', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),
     ('nw_execute_multi_scales', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),
+    ('nw_execute_multi_device', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, ctypes.POINTER(_P),
+                                               ctypes.POINTER(_I64), ctypes.POINTER(_P), ctypes.c_int]),
     ('nw_baseline', ctypes.c_int, [ctypes.c_int, ctypes.c_int, _P, _I64, _I64, _I64, _I64, ctypes.c_int, _P,
                                    ctypes.c_int, ctypes.POINTER(ctypes.c_double)]),
     ('nw_make_wavelets', ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.c_int,
@@ -84,6 +90,7 @@ SIGNATURES = [
                                         ctypes.c_double, _P, ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64)]),
     ('nw_plan_set_stream', ctypes.c_int, [_P, _P]),
+    ('nw_plan_get_stream', ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     ('nw_plan_sync', ctypes.c_int, [_P]),
     ('nw_plan_stats', ctypes.c_int, [_P, ctypes.POINTER(nw_stats)]),
     ('nw_plan_reset_stats', ctypes.c_int, [_P]),

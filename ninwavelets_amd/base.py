@@ -274,9 +274,12 @@ class WaveletBase:
         self._rows = None
 
     # ------------------------------------------------------------------ execution
-    def _plan(self, n: int, nsig: int, device: int, scales: tuple[int, int] | None = None) -> Plan:
+    def _plan(self, n: int, nsig: int, device: int, scales: tuple[int, int] | None = None,
+              slot: int = 0) -> Plan:
         """The cached plan for (n, batch, device) -- of the scale slice [f0, f1) when
-        ``scales`` is given (scale-sharded multi-device calls)."""
+        ``scales`` is given (scale-sharded multi-device calls).  ``slot`` is the shard
+        index of a multi-device call: a plan is not reentrant, so ``devices=[0, 0]`` gets
+        one plan per shard, never one plan driven from two host threads."""
         c = self._cache
         f0, f1 = scales if scales is not None else (0, len(c.freqs))
         nf = f1 - f0
@@ -287,7 +290,7 @@ class WaveletBase:
         while batch < min(nsig, cap):
             batch *= 2
         batch = min(batch, cap)
-        key = (n, nf, self.dtype.str, bool(self.interpolate), device, batch, self.engine, f0)
+        key = (n, nf, self.dtype.str, bool(self.interpolate), device, batch, self.engine, f0, slot)
         plan = self._plans.get(key)
         if plan is None:
             plan = Plan(n, nf, self.dtype, device, batch, self.interpolate, self.engine)
@@ -308,14 +311,14 @@ class WaveletBase:
         nf = len(self._cache.freqs)
         if len(devs) > 1 and nsig < len(devs) and nf >= len(devs):
             from .dist import shard
-            plans = [self._plan(n, nsig, d, shard(nf, i, len(devs))) for i, d in enumerate(devs)]
+            plans = [self._plan(n, nsig, d, shard(nf, i, len(devs)), slot=i) for i, d in enumerate(devs)]
             out = execute_multi(plans, x.reshape(nsig, n), out_kind, shard='scales')
             if out_kind in REDUCTIONS:
                 return out
             return out.reshape(x.shape[:-1] + out.shape[-2:])
         if len(devs) > 1 and nsig > 1:
-            per = -(-nsig // len(devs))
-            plans = [self._plan(n, per, d) for d in devs]
+            per = -(-nsig // len(devs))          # the largest balanced block (dist.shard)
+            plans = [self._plan(n, per, d, slot=i) for i, d in enumerate(devs)]
             out = execute_multi(plans, x.reshape(nsig, n), out_kind)
             if out_kind in REDUCTIONS:
                 return out

@@ -322,6 +322,7 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
         NW_TRY(ensure(&p->d_scratch, &p->d_scratch_bytes, nw::large_scratch_bytes(p->n, p->nfreq, p->dtype)));
         const size_t out_row = (size_t)p->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
         const int64_t fc = nw::large_fchunk(p->n, p->nfreq, p->dtype);
+        p->stats.kernel = NW_K_TWO_PASS;
         for (int64_t sidx = 0; sidx < c; ++sidx) {
             const char* Xs = (const char*)p->d_X + (size_t)sidx * p->nh * 2 * p->esz;
             char* os = (char*)dst + (size_t)sidx * p->nfreq * out_row;
@@ -346,6 +347,7 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
     if (!rocfft_engine && p->chirp) {
         // chirp-z form (any other n up to 8192 fp32 / 4096 fp64): two on-chip FFTs per row
         NW_TRY(chirp_table(p));
+        p->stats.kernel = NW_K_CHIRP;
         if (p->chirp)
             return staged(p, ST_FUSED, [&] {
                 NW_HIP(nw::launch_chirp(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->chirp_counts,
@@ -361,6 +363,7 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
             NW_HIP(nw::build_wtable(p->desc, p->dtype, p->d_wtab, p->stream));
             p->wtab_valid = true;
         }
+        p->stats.kernel = nw::fused_kernel_id(p->n, p->dtype, p->desc.kind);
         return staged(p, ST_FUSED, [&] {
             NW_HIP(nw::launch_fused(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->stream));
             return NW_OK;
@@ -373,6 +376,7 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
         NW_TRY(need_Y(p));
         Y = p->d_Y;
     }
+    p->stats.kernel = NW_K_MULTIPLY;
     NW_TRY(staged(p, ST_MUL, [&] {
         NW_HIP(nw::launch_multiply(p->desc, p->dtype, p->d_X, Y, c, p->stream));
         return NW_OK;
@@ -1103,6 +1107,31 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     return NW_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
+// Balanced contiguous blocks (dist.shard): nsig / n signals per device, one more for the
+// first nsig % n devices, so no device is idle while nsig >= n.
+void block_of(int64_t nsig, int i, int n, int64_t* s0, int64_t* cnt) {
+    const int64_t base = nsig / n, extra = nsig % n;
+    *s0 = (int64_t)i * base + std::min<int64_t>(i, extra);
+    *cnt = base + (i < extra ? 1 : 0);
+}
+
+// A plan is not reentrant: one host thread per plan, so a plan may appear only once.
+int check_distinct(nw_plan* const* plans, int nplans, const char* who) {
+    for (int i = 0; i < nplans; ++i) {
+        if (!plans[i]) return fail(NW_E_INVALID, std::string(who) + ": null plan");
+        for (int j = 0; j < i; ++j)
+            if (plans[j] == plans[i])
+                return fail(NW_E_INVALID, std::string(who) + ": plan " + std::to_string(i) +
+                                              " repeats plan " + std::to_string(j) +
+                                              " (a plan is not reentrant: create one plan per shard)");
+    }
+    return NW_OK;
+}
+
 // Reductions over devices: each device sums its contiguous block (fp64 partial sums),
 // the host adds them in device order, then takes the mean / |mean| exactly as
 // k_finalize does.
@@ -1113,14 +1142,13 @@ static int execute_multi_reduce(nw_plan* const* plans, int nplans, const void* x
     const int64_t fn = (int64_t)p0->nfreq * p0->n;
     const size_t comps = (size_t)fn * (phase ? 2 : 1);
     const size_t x_row = (size_t)p0->n * p0->esz;
-    const int64_t per = (nsig + nplans - 1) / nplans;
     std::vector<std::vector<double>> part(nplans);
     std::vector<int> rc(nplans, NW_OK);
     std::vector<std::string> err(nplans);
     std::vector<std::thread> th;
     for (int i = 0; i < nplans; ++i) {
-        const int64_t s0 = std::min<int64_t>(nsig, (int64_t)i * per);
-        const int64_t cnt = std::min<int64_t>(nsig, s0 + per) - s0;
+        int64_t s0 = 0, cnt = 0;
+        block_of(nsig, i, nplans, &s0, &cnt);
         if (cnt <= 0) continue;
         part[i].assign(comps, 0.0);
         th.emplace_back([&, i, s0, cnt] {
@@ -1150,24 +1178,33 @@ static int execute_multi_reduce(nw_plan* const* plans, int nplans, const void* x
     return NW_OK;
 }
 
+int check_same_config(nw_plan* const* plans, int nplans, const char* who) {
+    for (int i = 1; i < nplans; ++i)
+        if (plans[i]->n != plans[0]->n || plans[i]->nfreq != plans[0]->nfreq || plans[i]->dtype != plans[0]->dtype)
+            return fail(NW_E_INVALID, std::string(who) + ": plans must share n, nfreq and dtype");
+    return NW_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t nsig, void* out, int out_kind) {
     if (!plans || nplans < 1) return fail(NW_E_INVALID, "nw_execute_multi: no plans");
-    for (int i = 1; i < nplans; ++i)
-        if (!plans[i] || plans[i]->n != plans[0]->n || plans[i]->nfreq != plans[0]->nfreq ||
-            plans[i]->dtype != plans[0]->dtype)
-            return fail(NW_E_INVALID, "nw_execute_multi: plans must share n, nfreq and dtype");
+    NW_TRY(check_distinct(plans, nplans, "nw_execute_multi"));
+    NW_TRY(check_same_config(plans, nplans, "nw_execute_multi"));
     const nw_plan* p0 = plans[0];
     if (out_kind < NW_OUT_CWT || out_kind > NW_OUT_PHASE_SUM) return fail(NW_E_INVALID, "nw_execute_multi: bad out_kind");
+    if (nsig < 0) return fail(NW_E_INVALID, "nw_execute_multi: nsig < 0");
     if (is_reduction(out_kind)) return execute_multi_reduce(plans, nplans, x, nsig, out, out_kind);
     const size_t x_row = (size_t)p0->n * p0->esz;
     const size_t o_row = (size_t)p0->nfreq * p0->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p0->esz;
-    const int64_t per = (nsig + nplans - 1) / nplans;
     std::vector<int> rc(nplans, NW_OK);
     std::vector<std::string> err(nplans);
     std::vector<std::thread> th;
     for (int i = 0; i < nplans; ++i) {
-        const int64_t s0 = std::min<int64_t>(nsig, (int64_t)i * per);
-        const int64_t cnt = std::min<int64_t>(nsig, s0 + per) - s0;
+        int64_t s0 = 0, cnt = 0;
+        block_of(nsig, i, nplans, &s0, &cnt);
         if (cnt <= 0) continue;
         th.emplace_back([&, i, s0, cnt] {
             rc[i] = nw_execute(plans[i], (const char*)x + s0 * x_row, cnt, (char*)out + s0 * o_row, out_kind,
@@ -1182,9 +1219,101 @@ int nw_execute_multi(nw_plan* const* plans, int nplans, const void* x, int64_t n
     return NW_OK;
 }
 
+// Device-resident sharding (one process, one host thread per device).  Plan i
+// transforms its own device-resident block x[i] (nsig[i] signals) into out[i]; nothing
+// crosses PCIe.  Reductions: every device sums its block into fp64 partials, device 0
+// gathers them peer-to-peer, adds them in device order and finalises into out[0].
+int nw_execute_multi_device(nw_plan* const* plans, int nplans, const void* const* x, const int64_t* nsig,
+                            void* const* out, int out_kind) {
+    if (!plans || nplans < 1 || !x || !nsig || !out) return fail(NW_E_INVALID, "nw_execute_multi_device: null argument");
+    NW_TRY(check_distinct(plans, nplans, "nw_execute_multi_device"));
+    NW_TRY(check_same_config(plans, nplans, "nw_execute_multi_device"));
+    if (out_kind < NW_OUT_CWT || out_kind > NW_OUT_PHASE_SUM)
+        return fail(NW_E_INVALID, "nw_execute_multi_device: bad out_kind");
+    int64_t total = 0;
+    for (int i = 0; i < nplans; ++i) {
+        if (nsig[i] < 0) return fail(NW_E_INVALID, "nw_execute_multi_device: nsig < 0");
+        total += nsig[i];
+    }
+    const bool reduce = is_reduction(out_kind);
+    if (reduce && !out[0]) return fail(NW_E_INVALID, "nw_execute_multi_device: null out[0]");
+    nw_plan* p0 = plans[0];
+    const bool phase = is_phase(out_kind);
+    const int64_t fn = (int64_t)p0->nfreq * p0->n;
+    const size_t acc_bytes = (size_t)fn * (phase ? 2 : 1) * sizeof(double);
+    // reductions: per-device fp64 partial sums, then device 0's gather buffer
+    std::vector<void*> part(nplans, nullptr);
+    void* gather = nullptr;
+    auto release = [&] {
+        for (int i = 0; i < nplans; ++i)
+            if (part[i]) {
+                DeviceGuard g(plans[i]->device);
+                (void)hipFree(part[i]);
+            }
+        if (gather) {
+            DeviceGuard g(p0->device);
+            (void)hipFree(gather);
+        }
+    };
+    if (reduce) {
+        for (int i = 0; i < nplans; ++i) {
+            DeviceGuard g(plans[i]->device);
+            if (hipMalloc(&part[i], acc_bytes) != hipSuccess) {
+                release();
+                return fail(NW_E_NOMEM, "nw_execute_multi_device: partial-sum buffer");
+            }
+        }
+    }
+    std::vector<int> rc(nplans, NW_OK);
+    std::vector<std::string> err(nplans);
+    std::vector<std::thread> th;
+    for (int i = 0; i < nplans; ++i) {
+        th.emplace_back([&, i] {
+            nw_plan* p = plans[i];
+            rc[i] = nw_execute(p, x[i], nsig[i], reduce ? part[i] : out[i],
+                               reduce ? (phase ? NW_OUT_PHASE_SUM : NW_OUT_POWER_SUM) : out_kind, NW_MEM_DEVICE);
+            if (rc[i] == NW_OK) rc[i] = nw_plan_sync(p);
+            if (rc[i] != NW_OK) err[i] = g_last_error;
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int i = 0; i < nplans; ++i)
+        if (rc[i] != NW_OK) {
+            release();
+            return fail(rc[i], "device " + std::to_string(plans[i]->device) + ": " + err[i]);
+        }
+    if (!reduce) return NW_OK;
+    int r = NW_OK;
+    {
+        DeviceGuard g(p0->device);
+        auto hip = [&](hipError_t e, const char* what) {
+            if (e != hipSuccess && r == NW_OK)
+                r = fail(NW_E_HIP, std::string("nw_execute_multi_device: ") + what + ": " + hipGetErrorString(e));
+            return r == NW_OK;
+        };
+        const int64_t comps = fn * (phase ? 2 : 1);
+        double* acc = (double*)part[0];
+        if (nplans > 1) hip(hipMalloc(&gather, acc_bytes), "hipMalloc");
+        for (int i = 1; i < nplans && r == NW_OK; ++i) {
+            if (hip(hipMemcpyPeerAsync(gather, p0->device, part[i], plans[i]->device, acc_bytes, p0->stream), "peer copy"))
+                hip(nw::launch_add_f64(acc, (const double*)gather, comps, p0->stream), "add");
+        }
+        if (r == NW_OK) {
+            if (out_kind == NW_OUT_POWER_SUM || out_kind == NW_OUT_PHASE_SUM)
+                hip(hipMemcpyAsync(out[0], acc, acc_bytes, hipMemcpyDeviceToDevice, p0->stream), "copy");
+            else
+                hip(nw::launch_finalize(p0->dtype, phase, acc, out[0], fn, total, p0->stream), "finalize");
+        }
+        hip(hipStreamSynchronize(p0->stream), "sync");
+    }
+    release();
+    return r;
+}
+
 int nw_execute_multi_scales(nw_plan* const* plans, int nplans, const void* x, int64_t nsig, void* out,
                             int out_kind) {
     if (!plans || nplans < 1 || !plans[0]) return fail(NW_E_INVALID, "nw_execute_multi_scales: no plans");
+    NW_TRY(check_distinct(plans, nplans, "nw_execute_multi_scales"));
     const nw_plan* p0 = plans[0];
     for (int i = 1; i < nplans; ++i)
         if (!plans[i] || plans[i]->n != p0->n || plans[i]->dtype != p0->dtype ||
@@ -1394,6 +1523,12 @@ int nw_plan_set_stream(nw_plan* p, void* stream) {
     return NW_OK;
 }
 
+int nw_plan_get_stream(nw_plan* p, void** stream) {
+    if (!p || !stream) return fail(NW_E_INVALID, "nw_plan_get_stream: null argument");
+    *stream = (void*)p->stream;
+    return NW_OK;
+}
+
 int nw_plan_sync(nw_plan* p) {
     if (!p) return fail(NW_E_INVALID, "nw_plan_sync: null plan");
     DeviceGuard guard(p->device);
@@ -1413,10 +1548,11 @@ int nw_plan_reset_stats(nw_plan* p) {
     if (!p) return fail(NW_E_INVALID, "nw_plan_reset_stats: null plan");
     DeviceGuard guard(p->device);
     NW_TRY(resolve_timing(p));
-    const int64_t engine = p->stats.engine, uniq = p->stats.unique_rows;
+    const int64_t engine = p->stats.engine, uniq = p->stats.unique_rows, kernel = p->stats.kernel;
     p->stats = nw_stats{};
     p->stats.engine = engine;
     p->stats.unique_rows = uniq;
+    p->stats.kernel = kernel;
     return NW_OK;
 }
 

@@ -555,6 +555,16 @@ hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
     return hipGetLastError();
 }
 
+int fused_kernel_id(int64_t n, int dtype, int kind) {
+    const bool realw = kind != NW_TABLE;
+#define NW_KID(TY, NN, EE)                                                                      \
+    if (n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64))                                \
+        return (realw ? kPairMode<TY, EE, true> : kPairMode<TY, EE, false>) ? NW_K_FUSED_PAIR : NW_K_FUSED;
+    NW_FUSED_TABLE(NW_KID)
+#undef NW_KID
+    return NW_K_NONE;
+}
+
 hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
                         int64_t nsig, hipStream_t s) {
     const bool realw = d.kind != NW_TABLE;

@@ -133,6 +133,7 @@ hipError_t launch_accumulate(int dtype, int src_kind, const void* src, double* a
                              hipStream_t s);
 hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, int64_t fn, int64_t nsig,
                            hipStream_t s);
+hipError_t launch_add_f64(double* acc, const double* src, int64_t count, hipStream_t s);
 // WaveletMode.Normal rows built on the device (base.py:249-256): one row per freq, laid
 // out in the FFT scratch grouped by row length (off), m timeline samples between
 // `half` zeros on each side (len = m + 2*half), np.arange's fill (t0, t1, delta).
@@ -173,6 +174,7 @@ size_t     fused_wtable_bytes(int64_t n, int nfreq, int dtype, int kind);
 hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s);
 hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
                         int64_t nsig, hipStream_t s);
+int        fused_kernel_id(int64_t n, int dtype, int kind);   // NW_K_FUSED or NW_K_FUSED_PAIR
 hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 pi i j / n), cached per device
 
 // chirp-z engine (nw_chirp.hip): n not taken by the power-of-two kernels, 2n - 1 <= 16384

@@ -216,6 +216,19 @@ hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, in
     return hipGetLastError();
 }
 
+// acc[i] += src[i] (fp64 partial sums of several devices, added in device order)
+__global__ __launch_bounds__(256) void k_add_f64(double* __restrict__ acc, const double* __restrict__ src,
+                                                 int64_t count) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += stride) acc[i] += src[i];
+}
+
+hipError_t launch_add_f64(double* acc, const double* src, int64_t count, hipStream_t s) {
+    const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((count + 255) / 256, 256 * 32));
+    k_add_f64<<<blocks, 256, 0, s>>>(acc, src, count);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------
 // WaveletMode.Normal rows (base.py:249-256 with make_wavelet 346-359 and
 // _setup_waveletshape 196-216).  Row f of the FFT scratch: `half` zeros, the

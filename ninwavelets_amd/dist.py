@@ -24,12 +24,14 @@ _SUM_OF = {'power_mean': 'power_sum', 'itc': 'phase_sum',
 
 
 def shard(nsig: int, rank: int, world: int) -> tuple[int, int]:
-    """[s0, s1) of rank's contiguous block: ceil(nsig / world) signals per rank."""
+    """[s0, s1) of rank's contiguous block, balanced: nsig // world items per rank and one
+    more for the first nsig % world ranks, so no rank is empty while nsig >= world (the
+    same split nw_execute_multi / nw_execute_multi_scales use across devices)."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f'bad rank {rank} of {world}')
-    per = -(-nsig // world)
-    s0 = min(nsig, rank * per)
-    return s0, min(nsig, s0 + per)
+    base, extra = divmod(nsig, world)
+    s0 = rank * base + min(rank, extra)
+    return s0, s0 + base + (1 if rank < extra else 0)
 
 
 def finalize(kind: str, total: np.ndarray, nsig: int, dtype) -> np.ndarray:

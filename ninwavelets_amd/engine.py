@@ -8,6 +8,7 @@ the plan stream).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 
 import numpy as np
@@ -119,8 +120,9 @@ class Plan:
                 raise ValueError('device execute needs an output tensor')
             nsig = x.numel() // self.n
             self._check_device_buffers(x, out, nsig, out_kind)
-            L.check(L.lib().nw_execute(self._h, ctypes.c_void_p(x.data_ptr()), nsig,
-                                       ctypes.c_void_p(out.data_ptr()), kind, L.NW_MEM_DEVICE))
+            with self._ordered_with_torch(x.device):
+                L.check(L.lib().nw_execute(self._h, ctypes.c_void_p(x.data_ptr()), nsig,
+                                           ctypes.c_void_p(out.data_ptr()), kind, L.NW_MEM_DEVICE))
             return out
         x = np.ascontiguousarray(x, dtype=self.dtype)
         if x.shape[-1] != self.n:
@@ -137,8 +139,30 @@ class Plan:
                                    out.ctypes.data_as(ctypes.c_void_p), kind, L.NW_MEM_HOST))
         return out
 
+    def stream_ptr(self) -> int:
+        """The hipStream_t the plan launches on."""
+        h = ctypes.c_void_p()
+        L.check(L.lib().nw_plan_get_stream(self._h, ctypes.byref(h)))
+        return h.value or 0
+
+    @contextlib.contextmanager
+    def _ordered_with_torch(self, device):
+        """Order a device-tensor execute with torch's current stream on both sides: the
+        plan stream waits for the work that produced the input, and torch's stream waits
+        for the plan's kernels before anything later reads the output or the caching
+        allocator reuses either buffer."""
+        import torch
+        cur = torch.cuda.current_stream(device)
+        plan_stream = torch.cuda.ExternalStream(self.stream_ptr(), device=device)
+        plan_stream.wait_stream(cur)
+        try:
+            yield
+        finally:
+            cur.wait_stream(plan_stream)
+
     def execute_ptr(self, x_ptr: int, nsig: int, out_ptr: int, out_kind: str = 'cwt'):
-        """Raw device pointers on the plan's device (asynchronous on the plan stream)."""
+        """Raw device pointers on the plan's device (asynchronous on the plan stream; the
+        caller orders it against its own streams, e.g. with plan.sync())."""
         L.check(L.lib().nw_execute(self._h, ctypes.c_void_p(x_ptr), int(nsig), ctypes.c_void_p(out_ptr),
                                    OUT_KINDS[out_kind], L.NW_MEM_DEVICE))
 
@@ -214,6 +238,35 @@ def execute_multi(plans, x: np.ndarray, out_kind: str = 'cwt', shard: str = 'sig
     L.check(fn(arr, len(plans), x.ctypes.data_as(ctypes.c_void_p), nsig,
                out.ctypes.data_as(ctypes.c_void_p), OUT_KINDS[out_kind]))
     return out
+
+
+def execute_multi_device(plans, xs, outs, out_kind: str = 'cwt'):
+    """Device-resident sharding (nw_execute_multi_device): plan i transforms
+    the torch tensor xs[i] (on plan i's device, (nsig_i, n)) into outs[i]; for the
+    reductions outs[0] receives the (F, n) result over every signal of every device.
+    One host thread per device; returns when every device is done."""
+    if not (len(plans) == len(xs) == len(outs)):
+        raise ValueError('one input and one output tensor per plan')
+    red = out_kind in REDUCTIONS
+    nsig = []
+    for i, (p, x, o) in enumerate(zip(plans, xs, outs)):
+        ns = x.numel() // p.n
+        if red:
+            if i == 0:
+                p._check_device_buffers(x, o, ns, out_kind)
+        else:
+            p._check_device_buffers(x, o, ns, out_kind)
+        nsig.append(ns)
+    import torch
+    for p, x in zip(plans, xs):                 # inputs produced on torch's streams are complete
+        torch.cuda.current_stream(x.device).synchronize()
+    P = ctypes.c_void_p
+    arr = (P * len(plans))(*[p.handle.value for p in plans])
+    xa = (P * len(plans))(*[x.data_ptr() for x in xs])
+    oa = (P * len(plans))(*[(o.data_ptr() if o is not None else 0) for o in outs])
+    na = (ctypes.c_int64 * len(plans))(*nsig)
+    L.check(L.lib().nw_execute_multi_device(arr, len(plans), xa, na, oa, OUT_KINDS[out_kind]))
+    return outs[0] if red else outs
 
 
 def make_wavelets(kind: str, params, freqs, sfreq: float, real_wave_length: float, device: int = 0) -> list:

@@ -1,0 +1,64 @@
+"""bench.py's multi-rank plumbing on CPU (no GPU, no kernels): the launcher that starts
+N fresh ranks itself, the gloo process group, the barrier-bracketed timing and the
+MAX over ranks (the driver's N = 1, 2, 4, 8 runs take the same path with nccl)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def run(*args, env=None):
+    e = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    e.update(env or {})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'bench.py'), *args], capture_output=True,
+                       text=True, timeout=240, env=e)
+    return r
+
+
+@pytest.mark.parametrize('gpus', [1, 2, 3])
+def test_launcher_runs_n_ranks_dry(gpus):
+    r = run('--gpus', str(gpus), '--dry-run', '--steps', '3', '--warmup', '1')
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1                       # rank 0's line only
+    d = json.loads(lines[0])
+    assert d['n_gpus'] == gpus and d['steps'] == 3 and d['warmup'] == 1
+    assert d['config']['parallelism'] == f'dp{gpus}'
+    # rank r sleeps 10 ms * (r + 1) per step: the reported step is the slowest rank's
+    assert d['ms_per_step'] >= 10.0 * gpus * 0.95
+
+
+def test_world_size_mismatch_fails_loudly():
+    r = run('--gpus', '4', '--dry-run', env={'WORLD_SIZE': '2', 'RANK': '0', 'LOCAL_RANK': '0'})
+    assert r.returncode != 0
+    assert 'WORLD_SIZE' in r.stderr
+
+
+def test_pmc_traffic_needs_current_sources(tmp_path, monkeypatch):
+    """A committed PMC summary is attached only when its engine-source hash matches."""
+    h = bench.source_hash()
+    assert len(h) == 16 and h == bench.source_hash()
+    prof = tmp_path / 'profiles'
+    prof.mkdir()
+    cfg = {'chunk': 8, 'n': 4096, 'dtype': 'float32', 'out': 'power'}
+    (prof / 'pmc_cx_a.json').write_text(json.dumps({'kernel': 'k', 'hbm_bytes_per_launch': 5.0,
+                                                    'config': dict(cfg, src_hash='0' * 16)}))
+    monkeypatch.setattr(bench, 'ROOT', str(tmp_path))
+    monkeypatch.setattr(bench, 'source_hash', lambda: h)
+    assert bench.pmc_traffic('k', 'cx', 8, 'fused', 'float32', 'power', 4096) == (None, None)
+    (prof / 'pmc_cx_b.json').write_text(json.dumps({'kernel': 'k', 'hbm_bytes_per_launch': 7.0,
+                                                    'config': dict(cfg, src_hash=h)}))
+    got, src = bench.pmc_traffic('k', 'cx', 8, 'fused', 'float32', 'power', 4096)
+    assert got == 7.0 and src.endswith('pmc_cx_b.json')
+    assert bench.pmc_traffic('k', 'cx', 16, 'fused', 'float32', 'power', 4096) == (None, None)
+
+
+def test_cpu_model_is_reported():
+    assert isinstance(bench.cpu_model(), str) and bench.cpu_model()

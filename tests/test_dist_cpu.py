@@ -99,6 +99,20 @@ def test_shard_blocks_cover_every_signal_once():
         D.shard(4, 2, 2)
 
 
+def test_shard_is_balanced_and_never_empty():
+    """Every block holds nsig // world or one more item, so no rank (device, scale slice)
+    is empty while nsig >= world: e.g. 10 scales over 8 devices, 5 over 4."""
+    for nsig in range(0, 70):
+        for world in range(1, 10):
+            sizes = [b - a for a, b in (D.shard(nsig, r, world) for r in range(world))]
+            assert sum(sizes) == nsig
+            assert max(sizes) - min(sizes) <= 1
+            if nsig >= world:
+                assert min(sizes) >= 1, (nsig, world)
+    assert [D.shard(10, r, 8) for r in range(8)][-1] == (9, 10)
+    assert D.shard(5, 3, 4) == (4, 5)
+
+
 def test_finalize_matches_numpy_mean():
     rng = np.random.default_rng(0)
     c = rng.standard_normal((9, 3, 17)) + 1j * rng.standard_normal((9, 3, 17))

@@ -5,11 +5,16 @@ on gfx950 FETCH_SIZE reads half the bytes of a wide coalesced stream, so
 traffic = (2 * FETCH_SIZE + WRITE_SIZE) * 1024.
 
 usage: python tools/pmc_summary.py <pmc_dir> <out.json> <kernel-substring> [config-json]
+(the config records the engine-source hash; bench.py attaches the traffic only on a match)
 """
-import csv, glob, json, sys, collections
+import csv, glob, json, os, sys, collections
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402  (source_hash: the summary is valid for these engine sources only)
 
 pmc_dir, out, kname = sys.argv[1:4]
 config = json.loads(sys.argv[4]) if len(sys.argv) > 4 else {}
+config['src_hash'] = bench.source_hash()
 vals = collections.defaultdict(list)
 durs = []
 for f in sorted(glob.glob(f'{pmc_dir}/p*/pmc_counter_collection.csv')):
