@@ -109,7 +109,7 @@ def pmc_traffic(kernel, config, chunk, engine, dtype='float32', out=None, n=None
     return None, None
 
 
-def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0):
+def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0, piece_rows_log2=22):
     """The CPU oracle (numpy + scipy.fftpack, the reference's arithmetic) on one core.
     The wavelet rows are built untimed (reuse=True caches them in the reference); the
     timed work is fft(x) per signal, then pad_to + multiply + ifft (+ |.|^2) per piece
@@ -117,7 +117,7 @@ def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0):
     from oracle import nw_oracle as O
     rng = np.random.default_rng(0)
     t = np.arange(n) / 1000.
-    fc = int(max(2, min(len(freqs), (1 << 22) // n)))     # >= 2: freq_dist needs two (base.py:272)
+    fc = int(max(2, min(len(freqs), (1 << piece_rows_log2) // n)))     # >= 2: freq_dist needs two (base.py:272)
     pieces, rows_done, sigs, el = {}, 0, 0, 0.0
     while el < budget_s:
         x = np.sin(2 * np.pi * rng.uniform(1, 100) * t) + 0.1 * rng.standard_normal(n)
@@ -146,7 +146,8 @@ def cpu_baseline(kind, n, freqs, out_kind, budget_s=12.0):
 def _pool_worker(args):
     kind, n, freqs, out_kind, budget_s, seed = args
     import numpy as _np
-    r = cpu_baseline(kind, n, _np.asarray(freqs), out_kind, budget_s)
+    # 4x smaller pieces than the single-process leg: os.cpu_count() workers share host RAM
+    r = cpu_baseline(kind, n, _np.asarray(freqs), out_kind, budget_s, piece_rows_log2=20)
     return r['value'] * r['sample_seconds'], r['sample_seconds'], r['rows_done']
 
 
