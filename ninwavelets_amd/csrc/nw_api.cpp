@@ -505,25 +505,6 @@ constexpr size_t kPiece = size_t(64) << 20;
 #define NW_COPY_THREADS 8
 #endif
 
-void parallel_copy(char* dst, const char* src, size_t bytes) {
-    const size_t min_share = size_t(4) << 20;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t nth = std::min<size_t>(std::min<size_t>(NW_COPY_THREADS, hw), std::max<size_t>(1, bytes / min_share));
-    if (nth <= 1) {
-        std::memcpy(dst, src, bytes);
-        return;
-    }
-    const size_t share = (bytes + nth - 1) / nth;
-    std::vector<std::thread> th;
-    for (size_t i = 1; i < nth; ++i) {
-        const size_t off = i * share;
-        if (off >= bytes) break;
-        th.emplace_back([=] { std::memcpy(dst + off, src + off, std::min(share, bytes - off)); });
-    }
-    std::memcpy(dst, src, std::min(share, bytes));
-    for (auto& t : th) t.join();
-}
-
 int copy_out(nw_plan* p, char* dst, const char* src, size_t bytes) {
     if (!p->pinned[0]) {
         for (int i = 0; i < 2; ++i) {
@@ -542,7 +523,8 @@ int copy_out(nw_plan* p, char* dst, const char* src, size_t bytes) {
         if (i > 0) {                                  // piece i-1 landed: copy it out while piece i flies
             const size_t k = i - 1, off = k * kPiece;
             NW_HIP(hipEventSynchronize(p->pinned_ev[k & 1]));
-            parallel_copy(dst + off, (const char*)p->pinned[k & 1], std::min(kPiece, bytes - off));
+            nw::host::parallel_copy(dst + off, (const char*)p->pinned[k & 1], std::min(kPiece, bytes - off),
+                                   NW_COPY_THREADS);
         }
     }
     return NW_OK;
@@ -590,35 +572,10 @@ int nw_device_count(int* n) {
     return NW_OK;
 }
 
-// np.arange(0, total, one) length: ceil((stop - start) / step), as numpy's
-// _calc_length does for Python-float arguments (start = 0).
-static int64_t arange_len(double stop, double step) {
-    const double q = stop / step;
-    if (q == 0.0 && stop != 0.0) return std::signbit(q) ? 0 : 1;
-    if (!(q > 0.0)) return 0;
-    return (int64_t)std::ceil(q);
-}
-
-// np.arange(start, stop, step) length for start != 0
-static int64_t arange_len_from(double start, double stop, double step) {
-    const double q = (stop - start) / step;
-    if (!(q > 0.0)) return 0;
-    return (int64_t)std::ceil(q);
-}
-
 int nw_trans_grid(double real_length, double sfreq, int interpolate, nw_grid* g) {
     if (!g || !(real_length > 0.0) || !(sfreq > 0.0))
         return fail(NW_E_INVALID, "nw_trans_grid: need real_length > 0, sfreq > 0");
-    // make_fft_wavelet(freq, real_length) -> _setup_trans_shape(real_length, rl'):
-    //   one = 1 / real_length; total = sfreq / real_length * rl'   (base.py:191-194, 238-245)
-    const double rl = real_length;
-    const double one = 1.0 / rl;
-    const double rwl = interpolate ? rl / 2.0 : rl;
-    const double total = sfreq / rl * rwl;
-    const int64_t len = arange_len(total, one);
-    g->delta = one;
-    g->len_valid = len;
-    g->len_full = interpolate ? 2 * len : len;   // hstack with zeros(len(t)) (base.py:241-242)
+    nw::host::trans_grid(real_length, sfreq, interpolate != 0, &g->delta, &g->len_valid, &g->len_full);
     return NW_OK;
 }
 
@@ -703,39 +660,13 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
 static int build_normal_table(nw_plan* p, int kind, const double* params, int nparams, const double* freqs,
                               int64_t* lmax_out) {
     const int F = p->nfreq;
-    const double sigma = kind == NW_MEXICAN_HAT ? (nparams > 0 ? params[0] : 7.0) : 0.0;
-    const int o = kind == NW_MEXICAN_HAT ? 1 : 0;
-    const double sfreq = nparams > o ? params[o] : 1000.0;
-    const double rwl = nparams > o + 1 ? params[o + 1] : 1.0;
-    const double peak = kind == NW_MEXICAN_HAT ? std::sqrt(6.0) / M_PI / M_PI : 1.0;   // wavelets.py:227-228
-    std::vector<nw::NormalRow> rows(F);
+    std::vector<nw::NormalRow> rows;
+    int64_t lmax = 0, off = 0;
+    double sigma = 0.0;
+    if (!nw::host::normal_rows(kind == NW_MEXICAN_HAT, params, nparams, freqs, F, rows, &lmax, &off, &sigma))
+        return fail(NW_E_INVALID, "nw_plan_set_wavelet: negative padding (np.zeros of a negative size)");
     std::map<int64_t, std::vector<int>> by_len;
-    int64_t lmax = 0;
-    for (int f = 0; f < F; ++f) {
-        const double fr = freqs[f];
-        const double total = 1.0 / peak * fr * 2.0 * M_PI;
-        const double one = 1.0 / sfreq * 2.0 * M_PI * fr / peak;
-        const double t0 = -total / 2.0, stop = total / 2.0;
-        const int64_t m = arange_len_from(t0, stop, one);
-        const int64_t half = (int64_t)((sfreq * rwl - (double)m) / 2.0);
-        if (half < 0) return fail(NW_E_INVALID, "nw_plan_set_wavelet: negative padding (np.zeros of a negative size)");
-        nw::NormalRow r{};
-        r.m = m;
-        r.half = half;
-        r.len = m + 2 * half;
-        r.t0 = t0;
-        r.t1 = t0 + one;
-        r.delta = r.t1 - t0;
-        rows[f] = r;
-        by_len[r.len].push_back(f);
-        lmax = std::max(lmax, r.len);
-    }
-    int64_t off = 0;
-    for (auto& kv : by_len)
-        for (int f : kv.second) {
-            rows[f].off = off;
-            off += kv.first;
-        }
+    for (int f = 0; f < F; ++f) by_len[rows[f].len].push_back(f);
     const size_t tbytes = (size_t)F * lmax * 2 * p->esz;
     std::vector<int64_t> lens(F);
     for (int f = 0; f < F; ++f) lens[f] = rows[f].len;
@@ -809,68 +740,14 @@ static int setup_unique_rows(nw_plan* p, int kind, const double* freqs, const st
     if (p->d_rep) NW_HIP(hipFree(p->d_rep));
     p->d_ubuf = nullptr;
     p->d_rep = nullptr;
-    std::vector<int> rep(F);
-    std::vector<int> uniq;   // first scale of every distinct row, in order
-    if (kind == NW_SHANNON) {
-        std::fill(rep.begin(), rep.end(), 0);
-        uniq.push_back(0);
-    } else if (kind == NW_TABLE && host_table) {
-        // user rows: equal length and equal contents (hash, then compare)
-        const int64_t L = p->desc.len_full;
-        const double* t = (const double*)host_table;
-        std::unordered_map<uint64_t, std::vector<int>> seen;
-        for (int f = 0; f < F; ++f) {
-            const int64_t len = p->row_len_host.empty() ? L : p->row_len_host[f];
-            const unsigned char* b = (const unsigned char*)(t + (size_t)f * L * 2);
-            uint64_t h = 1469598103934665603ull ^ (uint64_t)len;   // FNV-1a over 8-byte words
-            for (size_t i = 0; i < (size_t)len * 2; ++i) {
-                uint64_t w;
-                std::memcpy(&w, b + 8 * i, 8);
-                h = (h ^ w) * 1099511628211ull;
-            }
-            int found = -1;
-            for (int g : seen[h]) {
-                const int64_t lg = p->row_len_host.empty() ? L : p->row_len_host[g];
-                if (lg == len && std::memcmp(b, t + (size_t)g * L * 2, (size_t)len * 16) == 0) {
-                    found = g;
-                    break;
-                }
-            }
-            if (found < 0) {
-                seen[h].push_back(f);
-                uniq.push_back(f);
-                rep[f] = f;
-            } else {
-                rep[f] = found;
-            }
-        }
-    } else {
-        // analytic kinds and Normal tables: a row is a function of its freq (bitwise)
-        std::unordered_map<uint64_t, int> first;
-        for (int f = 0; f < F; ++f) {
-            uint64_t key;
-            std::memcpy(&key, &freqs[f], sizeof(key));
-            auto it = first.find(key);
-            if (it == first.end()) {
-                first.emplace(key, f);
-                uniq.push_back(f);
-                rep[f] = f;
-            } else {
-                rep[f] = it->second;
-            }
-        }
-    }
+    const bool user_table = kind == NW_TABLE && host_table;
+    const nw::host::RowGroups groups =
+        nw::host::group_rows(kind == NW_SHANNON, F, freqs, user_table ? (const double*)host_table : nullptr,
+                             p->desc.len_full, user_table && !p->row_len_host.empty() ? p->row_len_host.data() : nullptr);
+    const std::vector<int>& uniq = groups.uniq;
     const int U = (int)uniq.size();
     if ((p->flags & NW_NO_DEDUP) || 2 * U > F) return NW_OK;
-    // scales grouped by distinct row: offs[u] .. offs[u + 1] index order[]
-    std::vector<int> uidx(F, -1), counts(U, 0);
-    for (int u = 0; u < U; ++u) uidx[uniq[u]] = u;
-    for (int f = 0; f < F; ++f) counts[uidx[rep[f]]]++;
-    std::vector<int32_t> host(U + 1 + F);
-    host[0] = 0;
-    for (int u = 0; u < U; ++u) host[u + 1] = host[u] + counts[u];
-    std::vector<int> fill(host.begin(), host.begin() + U);
-    for (int f = 0; f < F; ++f) host[U + 1 + fill[uidx[rep[f]]]++] = f;
+    const std::vector<int32_t>& host = groups.packed;
     // compacted per-freq arrays of the distinct rows
     const nw::WDesc& d = p->desc;
     const bool table = d.kind == NW_TABLE;
@@ -1111,13 +988,7 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
 
 namespace {
 
-// Balanced contiguous blocks (dist.shard): nsig / n signals per device, one more for the
-// first nsig % n devices, so no device is idle while nsig >= n.
-void block_of(int64_t nsig, int i, int n, int64_t* s0, int64_t* cnt) {
-    const int64_t base = nsig / n, extra = nsig % n;
-    *s0 = (int64_t)i * base + std::min<int64_t>(i, extra);
-    *cnt = base + (i < extra ? 1 : 0);
-}
+using nw::host::block_of;   // balanced contiguous blocks, as dist.shard
 
 // A plan is not reentrant: one host thread per plan, so a plan may appear only once.
 int check_distinct(nw_plan* const* plans, int nplans, const char* who) {
@@ -1433,7 +1304,7 @@ int nw_make_wavelets(int device, int kind, const double* params, int nparams, co
         nw::WaveRow r{};
         if (reverse) {                        // _setup_trans_shape(freq, real_wave_length), base.py:191-194
             const double one = 1.0 / fr;
-            r.m = arange_len(sfreq / fr * rwl, one);
+            r.m = nw::host::arange_len(sfreq / fr * rwl, one);
             r.len = 2 * (r.m / 2);
             r.t0 = 0.0;
             r.delta = one;
@@ -1445,7 +1316,7 @@ int nw_make_wavelets(int device, int kind, const double* params, int nparams, co
             const double total = 1.0 / peak * fr * 2.0 * M_PI;
             const double one = 1.0 / sfreq * 2.0 * M_PI * fr / peak;
             r.t0 = -total / 2.0;
-            r.m = arange_len_from(r.t0, total / 2.0, one);
+            r.m = nw::host::arange_len_from(r.t0, total / 2.0, one);
             r.len = r.m;
             r.t1 = r.t0 + one;
             r.delta = r.t1 - r.t0;

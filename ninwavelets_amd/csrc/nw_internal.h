@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include "../../include/ninwave.h"
+#include "nw_host.h"
 
 namespace nw {
 
@@ -137,10 +138,6 @@ hipError_t launch_add_f64(double* acc, const double* src, int64_t count, hipStre
 // WaveletMode.Normal rows built on the device (base.py:249-256): one row per freq, laid
 // out in the FFT scratch grouped by row length (off), m timeline samples between
 // `half` zeros on each side (len = m + 2*half), np.arange's fill (t0, t1, delta).
-struct NormalRow {
-    int64_t off, m, half, len;
-    double t0, t1, delta;
-};
 hipError_t launch_normal_time(const NormalRow* rows, int nrows, int64_t lmax, int kind, double sigma, void* buf,
                               hipStream_t s);
 hipError_t launch_normal_finish(const NormalRow* rows, int nrows, int64_t lmax, bool interp, const void* buf,

@@ -36,6 +36,21 @@ def load_golden(name):
     return d
 
 
+def long_signal(n: int, seed: int, sfreq: float = 1000.) -> np.ndarray:
+    """Input of the benchmark-length goldens (tests/golden/make_golden_long.py), rebuilt from
+    its seed: two sinusoids + 0.1 N(0, 1) noise from np.random.default_rng(seed)."""
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / sfreq
+    f1, f2 = rng.uniform(3, 120, 2)
+    return (np.sin(2 * np.pi * f1 * t) + 0.5 * np.sin(2 * np.pi * f2 * t + 1.0)
+            + 0.1 * rng.standard_normal(n))
+
+
+def x_digest(x: np.ndarray) -> str:
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(x, dtype=np.float64).tobytes()).hexdigest()
+
+
 @pytest.fixture(scope='session')
 def gpu_available():
     try:

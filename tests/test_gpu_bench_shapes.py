@@ -1,0 +1,116 @@
+"""GPU parity at the shapes the bench lines time (BASELINE.json configs C2-C5).
+
+- C3 as benchmarked: Morse POWER (and abs) at N = 4096, F = 256 (freqs 1..256), fp32, chunks
+  of >= 2 signals so ``nw_fused_pair_kernel`` runs with every pass-0 pruning variant
+  (reference: base.py:409-443 power/abs over base.py:378-407 cwt);
+- the same at N = 16384 (``nw_fused_kernel``, E = 32), power;
+- Shannon fp32 at N = 2^24 with 16 scales (the repeated-row path: one computed row and
+  ``k_expand_rows``; wavelets.py:256-262);
+- the reference's own outputs at the benchmark lengths (tests/golden/long_*.npz, made by
+  tests/golden/make_golden_long.py): N = 16384 (C2 Morlet, C4 Morse), 2^17 and 2^24 (C5).
+
+Tolerances as in test_gpu_parity.py: fp64 1e-12 of max|ref|; fp32 1e-5 (x2 for |.|^2) at
+N <= 16384, 1e-4 at N >= 2^17.
+"""
+import numpy as np
+import pytest
+
+from conftest import golden_names, load_golden, long_signal, x_digest
+from oracle import nw_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+import ninwavelets_amd as nw  # noqa: E402
+from ninwavelets_amd import _lib as L  # noqa: E402
+
+
+def synth(S, n, seed, sfreq=1000.):
+    rng = np.random.default_rng(seed)
+    t = np.arange(n) / sfreq
+    fc = rng.uniform(1, 100, (S, 1))
+    ph = rng.uniform(0, 2 * np.pi, (S, 1))
+    return (np.sin(2 * np.pi * fc * t + ph) + 0.1 * rng.standard_normal((S, n))).astype(np.float32)
+
+
+def plan_for(n, freqs, dtype, max_batch, kind='morse', params=(17.5, 3.), **kw):
+    g = L.trans_grid(n / 1000., 1000., False)
+    p = nw.Plan(n, len(freqs), dtype, max_batch=max_batch, **kw)
+    p.set_wavelet(kind, list(params), np.asarray(freqs, dtype=np.float64), g)
+    return p
+
+
+def max_err(got, ref):
+    return np.max(np.abs(got - ref)) / np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize('n,kernel', [(4096, 'nw_fused_pair_kernel'), (16384, 'nw_fused_kernel')])
+@pytest.mark.parametrize('out_kind', ['power', 'abs'])
+def test_bench_shape_power_abs_against_oracle(n, kernel, out_kind):
+    """Every one of the 256 scales of 4 signals (C3 / C4 scale list) in chunks of 2 and 4
+    signals, against the oracle's |cwt|^2 / |cwt|; the kernel that ran is the bench's."""
+    S, freqs = 4, np.arange(1, 257, dtype=np.float64)
+    x = synth(S, n, seed=n + 7)
+    ref = np.stack([O.cwt('morse', x[s].astype(np.float64), freqs) for s in range(S)])
+    ref = np.abs(ref) ** 2 if out_kind == 'power' else np.abs(ref)
+    for chunk in (2, 4):
+        plan = plan_for(n, freqs, 'float32', chunk)
+        got = plan.execute(x, out_kind=out_kind)
+        st = plan.stats()
+        assert st['engine'] == 'fused' and L.KERNEL_NAMES[st['kernel']] == kernel, st
+        assert got.shape == (S, 256, n) and got.dtype == np.float32
+        err = max_err(got, ref)
+        assert err <= (2e-5 if out_kind == 'power' else 1e-5), (chunk, err)
+        # each row against its own scale: the pruned (low-f) rows are tiny next to the max
+        for f in (0, 1, 3, 10, 40, 100, 255):
+            r = ref[:, f]
+            assert np.max(np.abs(got[:, f] - r)) <= 3e-5 * np.max(np.abs(r)) + 1e-30, (chunk, f)
+
+
+def test_c3_power_cwt_consistent_on_pair_kernel():
+    """C3's power output equals |cwt|^2 of the same kernel family's complex output."""
+    n, S, freqs = 4096, 8, np.arange(1, 257, dtype=np.float64)
+    x = synth(S, n, seed=99)
+    plan = plan_for(n, freqs, 'float32', 8)
+    c = plan.execute(x, out_kind='cwt').astype(np.complex128)
+    p = plan.execute(x, out_kind='power')
+    assert max_err(p, np.abs(c) ** 2) <= 4e-7
+
+
+def test_c5_shannon_fp32_16_scales():
+    """C5's Shannon line at 2^24 (fp32): 16 scales; Shannon ignores the freq, so one row is
+    computed and copied 15 times; every row against the oracle (tolerance 1e-4 at 2^24)."""
+    n, F = 1 << 24, 16
+    freqs = np.linspace(0.5, 250, 512)[::32]
+    x = synth(1, n, seed=5)[0]
+    w = nw.Shannon(1000, dtype='float32')
+    out = w.cwt(x, freqs)
+    assert out.shape == (F, n) and out.dtype == np.complex64
+    ref = O.cwt('shannon', x.astype(np.float64), freqs[:2])[0]
+    for f in range(F):
+        assert max_err(out[f], ref) <= 1e-4, f
+    assert all(np.array_equal(out[f], out[0]) for f in range(1, F))
+
+
+LONG = golden_names('long_')
+
+
+@pytest.mark.parametrize('dtype', ['float64', 'float32'])
+@pytest.mark.parametrize('name', LONG)
+def test_reference_outputs_at_benchmark_lengths(name, dtype):
+    """The drop-in cwt against the reference run at the benchmark lengths: the 2048 sampled
+    points of every scale, and each row's sum and energy (every output point)."""
+    g = load_golden(name)
+    m = g['meta']
+    n = m['n']
+    x = long_signal(n, m['seed'])
+    assert x_digest(x) == m['x_sha256']
+    cls = {'morse': nw.Morse, 'morlet': nw.Morlet}[m['kind']]
+    out = cls(m['sfreq'], dtype=dtype).cwt(x.astype(dtype), g['freqs'])
+    assert out.shape == (len(g['freqs']), n)
+    tol = 1e-12 if dtype == 'float64' else (1e-5 if n <= 16384 else 1e-4)
+    ref = g['out_at']
+    assert max_err(out[:, g['pos']], ref) <= tol
+    o = out.astype(np.complex128)
+    s_tol = tol * np.sqrt(n)         # sum of n independent rounding errors
+    assert np.max(np.abs(o.sum(axis=1) - g['row_sum'])) <= s_tol * np.max(np.abs(ref)) * np.sqrt(n)
+    np.testing.assert_allclose((np.abs(o) ** 2).sum(axis=1), g['row_energy'], rtol=4 * tol)

@@ -7,7 +7,7 @@ import pytest
 from conftest import golden_names, load_golden
 from oracle import nw_oracle as O
 
-SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets'))]
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets', 'long'))]
 
 
 def _params(meta):
@@ -89,3 +89,22 @@ def test_oracle_make_wavelets(name):
     for got, want in zip(rows, ref):
         assert got.shape == want.shape
         np.testing.assert_array_equal(got.astype(np.complex128), want)
+
+
+@pytest.mark.parametrize('name', golden_names('long_'))
+def test_oracle_matches_reference_at_benchmark_lengths(name):
+    """The oracle at the benchmark lengths (N = 16384 for C2/C4, 2^17, 2^24 for C5) against
+    the reference run at those lengths (tests/golden/make_golden_long.py): the sampled
+    output points bit-exact-level (<= 1e-15 of max|ref|), and every row's sum and energy."""
+    from conftest import long_signal, x_digest
+    g = load_golden(name)
+    m = g['meta']
+    x = long_signal(m['n'], m['seed'])
+    assert x_digest(x) == m['x_sha256']             # the same input the reference saw
+    out = O.cwt(m['kind'], x, g['freqs'], sfreq=m['sfreq'])
+    assert out.shape == (len(g['freqs']), m['n'])
+    ref = g['out_at']
+    assert np.max(np.abs(out[:, g['pos']] - ref)) <= 1e-15 * max(1.0, np.max(np.abs(ref)))
+    np.testing.assert_allclose(out.sum(axis=1), g['row_sum'], rtol=0,
+                               atol=1e-13 * np.max(np.abs(g['row_sum'])))
+    np.testing.assert_allclose((np.abs(out) ** 2).sum(axis=1), g['row_energy'], rtol=1e-13)
