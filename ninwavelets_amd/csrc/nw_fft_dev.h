@@ -26,6 +26,9 @@
 #define NW_PRUNE_MIN 4     // smallest pass-0 variant (support rounded up to it; 1 and 2 add
                            // code without a measurable gain)
 #endif
+#ifndef NW_SWZ_LAST
+#define NW_SWZ_LAST 1      // conflict-free paired last-pass reads at T = 512 (PassInfo::SWZ)
+#endif
 #ifndef NW_XDMA_MIN_E
 #define NW_XDMA_MIN_E 32 // fp32 with E >= this: the next signal's X copied into the idle LDS
                          // image by LDS-DMA before the stores (measured: E=32 1.99 -> 1.94 ms,
@@ -243,6 +246,26 @@ template <int N, int E> struct Geometry {
     }
 };
 
+// The image feeding pass P may use its own padding group PG (slots of 2 pad slots).
+// Signal-pair kernel at T = 256 (n = 4096, E = 16): pass 0 writes each lane's 16 slots as
+// 8 ds_write_b128 of 16 B; with 2 pad slots per 32 two lanes share a pad block, so lanes
+// t, t+1 of every 8-lane group hit the same banks (2-way on every pass-0 write,
+// SQ_LDS_BANK_CONFLICT 0.54 of LDS cycles at C3).  Padding the 0 -> 1 image per 16 slots
+// makes those writes conflict-free (stride 18 slots = 36 dwords per lane); pass 1's
+// lanes 16-31 of each 32-lane ds_read_b64 group then take the butterfly block 8 blocks
+// further (PassInfo::REMAP: 8 * 18 slots = 288 = 32 mod 64 dwords), so those reads stay
+// conflict-free too.  The 1 -> 2 image keeps 2 per 32 (its accesses are lane-contiguous).
+#ifndef NW_PAIR_PAD16
+#define NW_PAIR_PAD16 0   // conflict-free, but measured 1.4 % slower at C3 (1.234 -> 1.252 ms per launch): off
+#endif
+template <int PG> __device__ __forceinline__ int lds_idx_p(int i) { return i + 2 * (i / PG); }
+template <int PG> constexpr int lds_off_p(int c) { return c + 2 * (c / PG); }
+template <typename T> constexpr bool kIsPair = !std::is_same<T, Sc<T>>::value;
+template <typename T, int N, int E>
+constexpr bool kPad16 = NW_PAIR_PAD16 && kIsPair<T> && E == 16 && N / E == 256 && Geometry<N, E>::npass() > 2;
+template <typename T, int N, int E, int P> constexpr int kPadX = (kPad16<T, N, E> && P == 1) ? 16 : kPadG<E>;
+template <typename T, int N, int E> constexpr int kImgElems = kPad16<T, N, E> ? N + 2 * (N / 16) : lds_elems<N, E>();
+
 // output value of one point: y, |y| or |y|^2
 template <int OUT, typename T> struct OutT { using type = T; };
 template <typename T> struct OutT<NW_OUT_CWT, T> { using type = C2<T>; };
@@ -326,6 +349,8 @@ template <int COMP, typename T> __device__ __forceinline__ T& comp(C2<T>& c) {
     if constexpr (COMP == 0) return c.re; else return c.im;
 }
 
+template <int N, int E, int P, int OSZ = 8, bool PK = false> struct PassInfo;
+
 // ---- one component of the pass-P outputs -> LDS (P = 0: slots t*E + s, as pairs)
 template <typename T, int N, int E, int P, int COMP>
 __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
@@ -349,8 +374,9 @@ __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
         return;
     }
 #endif
+    constexpr int PG = kPadX<T, N, E, P + 1>;
     if constexpr (P == 0) {
-        Pair<T>* dst = reinterpret_cast<Pair<T>*>(lds + lds_idx<E>(t * E));
+        Pair<T>* dst = reinterpret_cast<Pair<T>*>(lds + lds_idx_p<PG>(t * E));
 #pragma unroll
         for (int u = 0; u < E / 2; ++u)
             dst[u] = Pair<T>{comp<COMP>(v[bitrev<E>(2 * u)]), comp<COMP>(v[bitrev<E>(2 * u + 1)])};
@@ -360,10 +386,11 @@ __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
         constexpr int Q = E / R;
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const int j = t + q * G::T;
-            T* dst = lds + lds_idx<E>((j / NS) * NS * R + j % NS);
+            // lane-contiguous butterflies (OSZ 16: never the paired last-pass order), or pass 1's remap
+            const int j = PassInfo<N, E, P, 16, kIsPair<T>>::bfly(t, q);
+            T* dst = lds + lds_idx_p<PG>((j / NS) * NS * R + j % NS);
 #pragma unroll
-            for (int i = 0; i < R; ++i) dst[lds_off<E>(bitrev<R>(i) * NS)] = comp<COMP>(v[q * R + i]);
+            for (int i = 0; i < R; ++i) dst[lds_off_p<PG>(bitrev<R>(i) * NS)] = comp<COMP>(v[q * R + i]);
         }
     }
 }
@@ -372,7 +399,7 @@ __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
 // in the LAST pass, where j = Q*t + q so a thread's outputs come in adjacent pairs.
 // OSZ: bytes of one output value (pairing is only worth it for outputs <= 8 B: a pair of
 // 16-B complex128 outputs is two 16-B stores per lane, each touching every other 16 B)
-template <int N, int E, int P, int OSZ = 8> struct PassInfo {
+template <int N, int E, int P, int OSZ, bool PK> struct PassInfo {
     using G = Geometry<N, E>;
     static constexpr int R = G::radix(P);
     static constexpr int NS = G::ns(P);
@@ -385,7 +412,21 @@ template <int N, int E, int P, int OSZ = 8> struct PassInfo {
     // n = 8192); the lane-contiguous j = t + q*T plus DPP packing keeps stores whole.
     static constexpr bool PAIRED = LAST && Q == 2 && OSZ <= 8;
     static_assert(STRIDE % E == 0 && NS % E == 0, "pad must stay linear");
-    __device__ static __forceinline__ int bfly(int t, int q) { return PAIRED ? Q * t + q : t + q * G::T; }
+    // Paired reads at T = 512 (n = 16384 fp32, E = 32; image padded 2 slots per 32): with
+    // lane-contiguous pairs j = 2t the second 16 lanes of every 32-lane ds_read_b64 group
+    // start 34 dwords after the first, so lane 31 lands on lane 0's banks 0-1: every read
+    // of the pass 2-way conflicted (SQ_LDS_BANK_CONFLICT 20 % of LDS cycles at C4).  Lanes
+    // 16-31 of each group take the pair block 16 blocks further (512 slots: 16 * 34 =
+    // 544 = 32 mod 64 dwords), so a group covers the 64 banks once.  Stores stay whole:
+    // each store instruction writes two 512-B runs.
+    static constexpr bool SWZ = PAIRED && NW_SWZ_LAST && G::T == 512 && kPadG<E> == 32;
+    // signal-pair kernel, n = 4096: pass 1 reads the per-16-padded image (see kPad16)
+    static constexpr bool REMAP = PK && NW_PAIR_PAD16 && P == 1 && !LAST && E == 16 && G::T == 256 && Q == 1;
+    __device__ static __forceinline__ int bfly(int t, int q) {
+        if constexpr (REMAP) return ((t >> 5) << 4) + (((t >> 4) & 1) << 7) + (t & 15);
+        if constexpr (SWZ) return 2 * (((t >> 5) << 4) + (((t >> 4) & 1) << 8) + (t & 15)) + q;
+        return PAIRED ? Q * t + q : t + q * G::T;
+    }
 };
 
 // Pass-1 twiddles w_{NS*R}^{(j % NS) * r} depend on j % NS only (NS = E, the pass-0
@@ -402,14 +443,14 @@ template <typename T, int N, int E> struct Tab1 {
     static constexpr int COUNT = Geometry<N, E>::npass() >= 2 ? NS * (R - 1) : 0;
     static constexpr bool ON = NW_TAB1 && COUNT > 0 && COUNT * (int)sizeof(C2<S>) <= 8192;
     static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<S>) : 0;
-    static_assert((lds_elems<N, E>() * sizeof(T)) % 16 == 0, "table alignment");
+    static_assert((kImgElems<T, N, E> * sizeof(T)) % 16 == 0, "table alignment");
     __device__ static __forceinline__ const C2<S>* table(const T* lds) {
-        return reinterpret_cast<const C2<S>*>(lds + lds_elems<N, E>());
+        return reinterpret_cast<const C2<S>*>(lds + kImgElems<T, N, E>);
     }
     // w_N^e entries from the exact table tw (tw[i] = exp(+2 pi i / N))
     __device__ static __forceinline__ void fill(T* lds, const C2<S>* __restrict__ tw, int t) {
         if constexpr (ON) {
-            C2<S>* tab = reinterpret_cast<C2<S>*>(lds + lds_elems<N, E>());
+            C2<S>* tab = reinterpret_cast<C2<S>*>(lds + kImgElems<T, N, E>);
             for (int i = t; i < COUNT; i += Geometry<N, E>::T) {
                 const int jj = i % NS, r = i / NS + 1;
                 tab[i] = tw[(jj * r * (N / (NS * R))) % N];
@@ -420,24 +461,25 @@ template <typename T, int N, int E> struct Tab1 {
 
 template <typename T, int N, int E, int P, int COMP, int OSZ>
 __device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
-    using I = PassInfo<N, E, P, OSZ>;
+    using I = PassInfo<N, E, P, OSZ, kIsPair<T>>;
     constexpr int R = I::R, Q = I::Q;
+    constexpr int PG = kPadX<T, N, E, P>;
     if constexpr (I::PAIRED) {
-        const T* src = lds + lds_idx<E>(Q * t);
+        const T* src = lds + lds_idx_p<PG>(I::bfly(t, 0));
 #pragma unroll
         for (int q = 0; q < Q; q += 2)
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const Pair<T> pr = *reinterpret_cast<const Pair<T>*>(src + q + lds_off<E>(r * I::STRIDE));
+                const Pair<T> pr = *reinterpret_cast<const Pair<T>*>(src + q + lds_off_p<PG>(r * I::STRIDE));
                 comp<COMP>(v[q * R + r]) = pr.a;
                 comp<COMP>(v[(q + 1) * R + r]) = pr.b;
             }
     } else {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
-            const T* src = lds + lds_idx<E>(t + q * Geometry<N, E>::T);
+            const T* src = lds + lds_idx_p<PG>(I::bfly(t, q));
 #pragma unroll
-            for (int r = 0; r < R; ++r) comp<COMP>(v[q * R + r]) = src[lds_off<E>(r * I::STRIDE)];
+            for (int r = 0; r < R; ++r) comp<COMP>(v[q * R + r]) = src[lds_off_p<PG>(r * I::STRIDE)];
         }
     }
 }
@@ -614,7 +656,7 @@ template <typename T, int E, bool REALW> constexpr bool kXDMA = sizeof(T) == 4 &
 #endif
 template <typename T, int N, int E> struct XBuf {
     static constexpr bool ON = NW_XBUF && E < 32 && E <= NW_WREG_MAX_E;
-    static constexpr int OFFSET = lds_elems<N, E>() * (int)sizeof(T) + Tab1<T, N, E>::BYTES;
+    static constexpr int OFFSET = kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES;
     static constexpr int BYTES = ON ? (N / 2) * (int)sizeof(C2<T>) : 0;
     static_assert(OFFSET % 16 == 0, "DMA alignment");
     __device__ static __forceinline__ C2<T>* at_lds(T* lds) {
@@ -622,7 +664,7 @@ template <typename T, int N, int E> struct XBuf {
     }
 };
 template <typename T, int N, int E> constexpr int kLdsBytes =
-    lds_elems<N, E>() * (int)sizeof(T) + Tab1<T, N, E>::BYTES + XBuf<T, N, E>::BYTES;
+    kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES + XBuf<T, N, E>::BYTES;
 
 
 // ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P.
@@ -641,7 +683,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
     using S = Sc<T>;
     constexpr bool PAIRSIG = !std::is_same<T, S>::value;
     constexpr int OSZ = (int)sizeof(typename OutT<OUT, S>::type);
-    using I = PassInfo<N, E, P, OSZ>;
+    using I = PassInfo<N, E, P, OSZ, kIsPair<T>>;
     if constexpr (P < Geometry<N, E>::npass()) {
         constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
         constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;

@@ -230,6 +230,11 @@ template <int KIND> struct RowW<double, KIND> {
 };
 
 // ---- pass 1: rows
+#ifndef NW_ROWS_XDMA
+#define NW_ROWS_XDMA 1   // fp32 E = 32 rows: pruned Xt rows by LDS-DMA ahead of the stores
+#endif
+// (analytic kinds only: table rows' wavelet_bin loads would exceed 128 VGPRs, as in nw_fused)
+template <typename T, int E, int KIND> constexpr bool kRowsXD = NW_ROWS_XDMA && sizeof(T) == 4 && E >= 32 && KIND != NW_TABLE;
 #define NW_LARGE_WPS 4
 #define NW_LARGE_WPS64 2   // fp64: twice the registers per element (as nw_fused)
 template <typename T, int N2, int E, int KIND>
@@ -261,20 +266,49 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_
 
     Tab1<T, N2, E>::fill(lds, tw, t);
     C2<T> x[E];
-    for (int k1 = rg * rgs; k1 < (rg + 1) * rgs; ++k1) {
-        // bins k = k1 + n1*k2 with k2 = t + r*T: rows r >= need are zero for every thread
-        const int need = km < k1 ? 1 : (km - k1) / n1 / G::T + 1;
+    // bins k = k1 + n1*k2 with k2 = t + r*T: elements r >= need are zero for every thread;
+    // pass 0 runs the variant NZ = nzv(need) elements
+    auto need_of = [&](int k1) { return km < k1 ? 1 : (km - k1) / n1 / G::T + 1; };
+    auto nzv_of = [](int need) { return need <= 4 ? 4 : need <= 8 ? 8 : (E > 16 && need <= 16) ? 16 : E; };
+    // XD: a row whose pass 0 reads only Xt[k1][0 .. N2/2) (NZ <= E/2) gets those bins by
+    // LDS-DMA into the idle image, issued BEFORE the previous row's stores (as nw_fused's
+    // next-signal X): global loads issued after the stores would wait for all of them in
+    // the in-order vmcnt queue
+    constexpr bool XD = kRowsXD<T, E, KIND>;
+    const int k1_begin = rg * rgs, k1_end = (rg + 1) * rgs;
+    bool in_lds = false;
+    if constexpr (XD) {
+        const int nz0 = nzv_of(need_of(k1_begin));
+        if (nz0 <= E / 2) {
+            dma_x<T, N2, G::T>(Xt + (int64_t)k1_begin * N2, lds, t, nz0 / 2);
+            in_lds = true;
+        }
+    }
+    for (int k1 = k1_begin; k1 < k1_end; ++k1) {
+        const int need = need_of(k1);
         const C2<T>* xrow = Xt + (int64_t)k1 * N2;
         const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(C2<T>);
         C2<T> v[E];
-        auto pass0 = [&]<int NZ>() {
+        if constexpr (XD) {
+            if (in_lds) {
+                // this wave's DMA landed (only the stores issued after it may be pending), then every wave's
+                if (k1 == k1_begin) wait_vmcnt<0>(); else wait_vmcnt<LastStores<T, N2, E, NW_OUT_CWT>::COUNT>();
+                lds_barrier();
+            }
+        }
+        auto pass0 = [&]<int NZ, bool FROM_LDS>() {
             int j0 = k1 + n1 * t;                  // bin k of element 0 (k2 = t)
             if constexpr (KIND != NW_TABLE) j0 -= wf.off;
             asm volatile("" : "+v"(j0));
+            int tl = t;                            // opaque here: LDS reads must not hoist above the dispatch
+            asm volatile("" : "+v"(tl));
+            const C2<T>* xl = reinterpret_cast<const C2<T>*>(lds);
 #pragma unroll
             for (int r = 0; r < E; ++r) {
                 if (r < NZ) {
-                    const C2<T> xv = *at(xrow, xo, (uint32_t)(r * G::T * sizeof(C2<T>)));
+                    C2<T> xv;
+                    if constexpr (FROM_LDS) xv = xl[tl + r * G::T];
+                    else xv = *at(xrow, xo, (uint32_t)(r * G::T * sizeof(C2<T>)));
                     const int j = j0 + r * n1 * G::T;
                     if constexpr (KIND == NW_TABLE) {
                         const cplx<T> w = wavelet_bin<T>(d, fi, (int64_t)j);
@@ -293,12 +327,30 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_
             }
             idft_br<T, E, NZ>(v);
         };
-        if (need <= 4) pass0.template operator()<4>();
-        else if (need <= 8) pass0.template operator()<8>();
-        else if (E > 16 && need <= 16) pass0.template operator()<(E > 16 ? 16 : E)>();
-        else pass0.template operator()<E>();
+        if (XD && in_lds) {
+            if (need <= 4) pass0.template operator()<4, XD>();
+            else if (need <= 8) pass0.template operator()<8, XD>();
+            else pass0.template operator()<(E > 16 ? 16 : E), XD>();
+        } else {
+            if (need <= 4) pass0.template operator()<4, false>();
+            else if (need <= 8) pass0.template operator()<8, false>();
+            else if (E > 16 && need <= 16) pass0.template operator()<(E > 16 ? 16 : E), false>();
+            else pass0.template operator()<E, false>();
+        }
         void* orow = B + ((int64_t)fl * n1 + k1) * N2;
-        passes_from<T, N2, E, NW_OUT_CWT, 1, false>(v, lds, t, tw, x, nullptr, orow, nullptr);
+        const C2<T>* xs_next = nullptr;
+        int rounds_next = 0;
+        if constexpr (XD) {
+            if (k1 + 1 < k1_end) {
+                const int nzn = nzv_of(need_of(k1 + 1));
+                if (nzn <= E / 2) {
+                    xs_next = Xt + (int64_t)(k1 + 1) * N2;
+                    rounds_next = nzn / 2;
+                }
+            }
+            in_lds = xs_next != nullptr;
+        }
+        passes_from<T, N2, E, NW_OUT_CWT, 1, XD>(v, lds, t, tw, x, xs_next, orow, nullptr, nullptr, rounds_next);
     }
 }
 
