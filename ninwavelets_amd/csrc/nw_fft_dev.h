@@ -436,12 +436,18 @@ template <int N, int E, int P, int OSZ, bool PK> struct PassInfo {
 #ifndef NW_TAB1
 #define NW_TAB1 1
 #endif
+#ifndef NW_TAB1_64
+#define NW_TAB1_64 0
+#endif
 template <typename T, int N, int E> struct Tab1 {
     using I = PassInfo<N, E, 1>;
     using S = Sc<T>;                                // entries in the scalar type (shared by a pair)
     static constexpr int NS = I::NS, R = I::R;
     static constexpr int COUNT = Geometry<N, E>::npass() >= 2 ? NS * (R - 1) : 0;
-    static constexpr bool ON = NW_TAB1 && COUNT > 0 && COUNT * (int)sizeof(C2<S>) <= 8192;
+    // fp64 at n = 16384: one block per CU whatever the table costs (256 VGPRs), and image +
+    // table (155 KiB) fit the CU's LDS
+    static constexpr bool ON = NW_TAB1 && COUNT > 0 &&
+                               (COUNT * (int)sizeof(C2<S>) <= 8192 || (NW_TAB1_64 && sizeof(S) == 8 && N == 16384));
     static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<S>) : 0;
     static_assert((kImgElems<T, N, E> * sizeof(T)) % 16 == 0, "table alignment");
     __device__ static __forceinline__ const C2<S>* table(const T* lds) {
@@ -645,7 +651,15 @@ struct LastStores {
 #endif
 
 // complex W rows (tables) keep the register path: with LDS-DMA they exceed 128 VGPRs
-template <typename T, int E, bool REALW> constexpr bool kXDMA = sizeof(T) == 4 && E >= NW_XDMA_MIN_E && REALW;
+#ifndef NW_XDMA64
+#define NW_XDMA64 1   // fp64 E = 32 too: n = 16384 fp64 cwt 10.90 -> 9.88 ms per 512-signal launch (one box)
+#endif
+template <typename T, int E, bool REALW>
+constexpr bool kXDMA = (sizeof(T) == 4 || NW_XDMA64) && E >= NW_XDMA_MIN_E && REALW;
+// DMA rounds (T lanes x 16 B each) holding the first nz pass-0 elements (T bins each)
+template <typename T> __device__ __forceinline__ int dma_rounds_for(int nz) {
+    return (nz * (int)sizeof(C2<T>) + 15) / 16;
+}
 
 // E = 16 (n <= 8192): X gets its OWN LDS buffer after the image and the pass-1 table, so
 // the next signal's X is DMA'd right after this signal's pass 0 and has the whole signal

@@ -72,6 +72,12 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
 #ifndef NW_DMA_PRUNE
 #define NW_DMA_PRUNE 1   // LDS-DMA of X limited to the pruned pass 0's bins
 #endif
+#ifndef NW_WKEEP32
+#define NW_WKEEP32 16   // measured C4: 0 / 8 / 16 -> 3.537 / 3.486 / 3.456 ms per launch (one box)
+#endif
+#ifndef NW_WKEEP64
+#define NW_WKEEP64 0
+#endif
 #ifndef NW_GROUP
 #define NW_GROUP 8   // measured: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (with NW_TILEG 4)
 #endif
@@ -136,8 +142,18 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
 #pragma unroll
         for (int r = 0; r < E; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
     }
+    // E = 32: the first WKEEP elements of W stay in registers for the block (a row pruned to
+    // NZ <= WKEEP reads no W per signal; loads issued after the previous signal's stores
+    // wait for all of them in the in-order vmcnt queue)
+    constexpr int WKEEP = (!WREG && REALW) ? (sizeof(T) == 4 ? NW_WKEEP32 : NW_WKEEP64) : 0;
+    WT wk[WKEEP > 0 ? WKEEP : 1];
+    if constexpr (WKEEP > 0) {
+#pragma unroll
+        for (int r = 0; r < WKEEP; ++r) wk[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
+    }
     auto w_at = [&](int r) -> WT {
         if constexpr (WREG) return w[r];
+        else if (r < WKEEP) return wk[r < WKEEP ? r : 0];
         else return *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
     };
 
@@ -162,7 +178,7 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
         const int nzv0 = nz0 < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz0;
         dma_x<T, N, G::T>(reinterpret_cast<const C2<T>*>(X + s_begin * d.nh),
                           XD ? (void*)lds : (void*)XBuf<T, N, E>::at_lds(lds), t,
-                          (XD && NW_DMA_PRUNE && nzv0 <= E / 2) ? (nzv0 + 1) / 2 : 1 << 30);
+                          (XD && NW_DMA_PRUNE && nzv0 <= E / 2) ? dma_rounds_for<T>(nzv0) : 1 << 30);
     }
     // W row support (device-built with the table): elements r >= nz of pass 0 multiply an
     // exactly-zero W for every thread of the block (k = t + r*T beyond the row's last
@@ -171,7 +187,7 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     // LDS-DMA only the X bins the pruned pass 0 reads: variant NZ (>= 4) reads bins < NZ*T,
     // i.e. NZ/2 rounds of 2*T bins, when it reads no mirrored bin (NZ <= E/2)
     const int nzv = nz < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz;
-    const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? (nzv + 1) / 2 : 1 << 30;
+    const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? dma_rounds_for<T>(nzv) : 1 << 30;
     for (int64_t s = s_begin; s < s_end; ++s) {
         const C2<T>* xl = nullptr;
         if constexpr (XD || XB) {
