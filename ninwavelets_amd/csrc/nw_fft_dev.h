@@ -693,7 +693,8 @@ template <typename T, int N, int E> constexpr int kLdsBytes =
 template <typename T, int N, int E, int OUT, int P, bool XD>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
-                                            Stamps* st, void* ocur2 = nullptr, int dma_rounds = 1 << 30) {
+                                            Stamps* st, void* ocur2 = nullptr, int dma_rounds = 1 << 30,
+                                            const void* xs_next2 = nullptr) {
     using S = Sc<T>;
     constexpr bool PAIRSIG = !std::is_same<T, S>::value;
     constexpr int OSZ = (int)sizeof(typename OutT<OUT, S>::type);
@@ -734,7 +735,14 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
         if constexpr (I::LAST && XD) {
             if (xs_next) {                     // the image is idle once every wave has read it
                 lds_barrier();
-                dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t, dma_rounds);
+                if constexpr (PAIRSIG) {       // two signals' half spectra, side by side
+                    dma_x<S, N, Geometry<N, E>::T>(reinterpret_cast<const C2<S>*>(xs_next), lds, t, dma_rounds);
+                    if (xs_next2)
+                        dma_x<S, N, Geometry<N, E>::T>(reinterpret_cast<const C2<S>*>(xs_next2),
+                                                       reinterpret_cast<C2<S>*>(lds) + N / 2, t, dma_rounds);
+                } else {
+                    dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t, dma_rounds);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -798,7 +806,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                 LastStores<T, N, E, OUT>::all(v, ocur, t);
             }
         } else {
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds);
+            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, xs_next2);
         }
     }
 }

@@ -260,6 +260,9 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
 #ifndef NW_PAIR
 #define NW_PAIR 1
 #endif
+#ifndef NW_PAIR_XDMA
+#define NW_PAIR_XDMA 0   // measured slower: C3 1.257 -> 1.356 ms, n = 1024 / 2048 +4 % (as the single-signal E = 16 XD)
+#endif
 #ifndef NW_WPS_PAIR
 #define NW_WPS_PAIR 4
 #endif
@@ -294,14 +297,59 @@ __global__ __launch_bounds__(N / E, NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc
     Tab1<f2, N, E>::fill(lds, tw, t);
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<float>) : sizeof(float));
     const int nz = NW_PRUNE ? wnz[fi] : E;
+    // PXD: the next pair's two half spectra X[0 .. N/2) are LDS-DMA'd side by side into the
+    // idle image before this pair's stores (as nw_fused_kernel's XD; the pair image of
+    // N + N/16 8-B slots holds both), the real Nyquist bins ride one pair ahead in registers
+    constexpr bool PXD = NW_PAIR_XDMA;
+    const int nzv = nz < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz;
+    const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? dma_rounds_for<float>(nzv) : 1 << 30;
+    C2<float> nyqa{0.0f, 0.0f}, nyqb{0.0f, 0.0f};
+    auto xrow = [&](int64_t s) { return reinterpret_cast<const C2<float>*>(X + s * d.nh); };
+    if constexpr (PXD) {
+        const int64_t s2 = s_begin + 1 < s_end ? s_begin + 1 : s_begin;
+        nyqa = xrow(s_begin)[N / 2];
+        nyqb = xrow(s2)[N / 2];
+        dma_x<float, N, G::T>(xrow(s_begin), lds, t, dma_rounds);
+        dma_x<float, N, G::T>(xrow(s2), reinterpret_cast<C2<float>*>(lds) + N / 2, t, dma_rounds);
+    }
     for (int64_t s = s_begin; s < s_end; s += 2) {
         const bool two = s + 1 < s_end;
         const int64_t s2 = two ? s + 1 : s;
         C2<f2> v[E];
+        if constexpr (PXD) {
+            // this wave's DMAs landed (only the previous pair's stores may be pending), then every wave's
+            if (s == s_begin) wait_vmcnt<0>(); else wait_vmcnt<2 * LastStores<float, N, E, OUT>::COUNT>();
+            lds_barrier();
+        }
         auto pass0 = [&]<int NZ>() {
             C2<float> xa[E], xb[E];
-            load_x<float, N, E, NZ>(xa, reinterpret_cast<const C2<float>*>(X + s * d.nh), t);
-            load_x<float, N, E, NZ>(xb, reinterpret_cast<const C2<float>*>(X + s2 * d.nh), t);
+            if constexpr (PXD) {
+                int tl = t;                    // opaque: the LDS reads must not hoist above the dispatch
+                asm volatile("" : "+v"(tl));
+                const C2<float>* la = reinterpret_cast<const C2<float>*>(lds);
+                const C2<float>* lb = la + N / 2;
+                const C2<float>* ma = la + (N - (E - 1) * G::T - tl);   // X[N - k], r >= E/2: one base,
+                const C2<float>* mb = lb + (N - (E - 1) * G::T - tl);   // positive immediates
+#pragma unroll
+                for (int r = 0; r < NZ; ++r) {
+                    if (r < E / 2) {
+                        xa[r] = la[tl + r * G::T];
+                        xb[r] = lb[tl + r * G::T];
+                    } else {                   // k = N/2 (t = 0, r = E/2) is the Nyquist bin
+                        xa[r] = ma[(E - 1 - r) * G::T];
+                        xb[r] = mb[(E - 1 - r) * G::T];
+                        if (r == E / 2 && t == 0) {
+                            xa[r] = nyqa;
+                            xb[r] = nyqb;
+                        }
+                        xa[r].im = -xa[r].im;
+                        xb[r].im = -xb[r].im;
+                    }
+                }
+            } else {
+                load_x<float, N, E, NZ>(xa, xrow(s), t);
+                load_x<float, N, E, NZ>(xb, xrow(s2), t);
+            }
 #pragma unroll
             for (int r = 0; r < E; ++r)
                 v[r] = r < NZ ? C2<f2>{f2{w[r] * xa[r].re, w[r] * xb[r].re}, f2{w[r] * xa[r].im, w[r] * xb[r].im}}
@@ -313,9 +361,21 @@ __global__ __launch_bounds__(N / E, NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc
         else if (nz <= 4) pass0.template operator()<4>();
         else if (nz <= 8) pass0.template operator()<8>();
         else pass0.template operator()<E>();
+        const C2<float>* xn1 = nullptr;
+        const C2<float>* xn2 = nullptr;
+        if constexpr (PXD) {
+            if (s + 2 < s_end) {
+                const int64_t n1 = s + 2, n2 = s + 3 < s_end ? s + 3 : s + 2;
+                xn1 = xrow(n1);
+                xn2 = xrow(n2);
+                nyqa = xn1[N / 2];
+                nyqb = xn2[N / 2];
+            }
+        }
         void* o1 = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;
         void* o2 = two ? (void*)((char*)out + (s2 * d.nfreq + fi) * (int64_t)N * out_esz) : nullptr;
-        passes_from<f2, N, E, OUT, 1, false>(v, lds, t, tw, nullptr, nullptr, o1, nullptr, o2);
+        passes_from<f2, N, E, OUT, 1, PXD>(v, lds, t, tw, nullptr, reinterpret_cast<const C2<f2>*>(xn1), o1,
+                                           nullptr, o2, dma_rounds, xn2);
     }
 }
 
