@@ -88,8 +88,16 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
 #define NW_TILEF 8
 #endif
 constexpr int kGroup = NW_GROUP;   // signals per block
-constexpr int kTileF = NW_TILEF;   // scales per XCD tile
-constexpr int kTileG = NW_TILEG;   // signal groups per XCD tile
+// XCD tile (scales x signal groups) per element type: fp64 runs one block per CU, so one
+// round of an XCD (32 blocks) is the whole tile
+#ifndef NW_TILEF64
+#define NW_TILEF64 NW_TILEF
+#endif
+#ifndef NW_TILEG64
+#define NW_TILEG64 NW_TILEG
+#endif
+template <typename T> constexpr int kTileFT = sizeof(T) == 8 ? NW_TILEF64 : NW_TILEF;   // scales per XCD tile
+template <typename T> constexpr int kTileGT = sizeof(T) == 8 ? NW_TILEG64 : NW_TILEG;   // signal groups per XCD tile
 
 #ifndef NW_WPS32
 #define NW_WPS32 4
@@ -119,6 +127,7 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     // kTileF scales x kTileG signal groups, so each W row is read by kTileG blocks
     // and each X group by kTileF blocks from L2 (W + X of a tile ~2.5 MiB), and
     // the XCD sweeps all scales of its groups before moving on.
+    constexpr int kTileF = kTileFT<T>, kTileG = kTileGT<T>;
     const int b = blockIdx.x;
     const int xcd = b & 7;
     const int local = b >> 3;
@@ -277,6 +286,7 @@ __global__ __launch_bounds__(N / E, NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc
     f2* lds = reinterpret_cast<f2*>(smem);
     const int t = threadIdx.x;
     // XCD-aware block -> (scale, signal group): as nw_fused_kernel
+    constexpr int kTileF = kTileFT<float>, kTileG = kTileGT<float>;
     const int b = blockIdx.x;
     const int xcd = b & 7;
     const int local = b >> 3;
@@ -491,6 +501,7 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
+    constexpr int kTileF = kTileFT<T>, kTileG = kTileGT<T>;
     const int64_t nsg = (nsig + kGroup - 1) / kGroup;
     const int64_t nsg_pad = (nsg + 8 * kTileG - 1) / (8 * kTileG) * (8 * kTileG);
     const int64_t nfr = (d.nfreq + kTileF - 1) / kTileF;

@@ -234,7 +234,11 @@ template <int KIND> struct RowW<double, KIND> {
 #define NW_ROWS_XDMA 1   // fp32 E = 32 rows: pruned Xt rows by LDS-DMA ahead of the stores
 #endif
 // (analytic kinds only: table rows' wavelet_bin loads would exceed 128 VGPRs, as in nw_fused)
-template <typename T, int E, int KIND> constexpr bool kRowsXD = NW_ROWS_XDMA && sizeof(T) == 4 && E >= 32 && KIND != NW_TABLE;
+#ifndef NW_ROWS_XDMA64
+#define NW_ROWS_XDMA64 0
+#endif
+template <typename T, int E, int KIND>
+constexpr bool kRowsXD = NW_ROWS_XDMA && (sizeof(T) == 4 || NW_ROWS_XDMA64) && E >= 32 && KIND != NW_TABLE;
 #define NW_LARGE_WPS 4
 #define NW_LARGE_WPS64 2   // fp64: twice the registers per element (as nw_fused)
 template <typename T, int N2, int E, int KIND>
@@ -280,7 +284,7 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_
     if constexpr (XD) {
         const int nz0 = nzv_of(need_of(k1_begin));
         if (nz0 <= E / 2) {
-            dma_x<T, N2, G::T>(Xt + (int64_t)k1_begin * N2, lds, t, nz0 / 2);
+            dma_x<T, N2, G::T>(Xt + (int64_t)k1_begin * N2, lds, t, dma_rounds_for<T>(nz0));
             in_lds = true;
         }
     }
@@ -345,7 +349,7 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_
                 const int nzn = nzv_of(need_of(k1 + 1));
                 if (nzn <= E / 2) {
                     xs_next = Xt + (int64_t)(k1 + 1) * N2;
-                    rounds_next = nzn / 2;
+                    rounds_next = dma_rounds_for<T>(nzn);
                 }
             }
             in_lds = xs_next != nullptr;
