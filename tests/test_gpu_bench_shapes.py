@@ -114,3 +114,40 @@ def test_reference_outputs_at_benchmark_lengths(name, dtype):
     s_tol = tol * np.sqrt(n)         # sum of n independent rounding errors
     assert np.max(np.abs(o.sum(axis=1) - g['row_sum'])) <= s_tol * np.max(np.abs(ref)) * np.sqrt(n)
     np.testing.assert_allclose((np.abs(o) ** 2).sum(axis=1), g['row_energy'], rtol=4 * tol)
+
+
+@pytest.mark.parametrize('n', [1201, 4097])
+def test_mne_lengths_power_all_scales(n):
+    """MNE epoch lengths (tmin..tmax inclusive) at the C3 scale list: the chirp-z form, Morse
+    power at all 256 scales of 4 signals in chunks of 2 (tolerance 2e-5 x2 for |.|^2, as
+    test_gpu_chirp.py)."""
+    S, freqs = 4, np.arange(1, 257, dtype=np.float64)
+    x = synth(S, n, seed=n)
+    ref = np.abs(np.stack([O.cwt('morse', x[s].astype(np.float64), freqs) for s in range(S)])) ** 2
+    plan = plan_for(n, freqs, 'float32', 2)
+    got = plan.execute(x, out_kind='power')
+    assert L.KERNEL_NAMES[plan.stats()['kernel']] == 'nw_chirp_kernel'
+    assert max_err(got, ref) <= 4e-5
+
+
+@pytest.mark.parametrize('out_kind', ['power', 'abs'])
+def test_c2_morlet_outputs_all_scales(out_kind):
+    """C2's wavelet (Morlet sigma = 7) at N = 16384, freqs 1..128, |.| and |.|^2 outputs."""
+    S, n, freqs = 2, 16384, np.arange(1, 129, dtype=np.float64)
+    x = synth(S, n, seed=77)
+    ref = np.stack([O.cwt('morlet', x[s].astype(np.float64), freqs) for s in range(S)])
+    ref = np.abs(ref) ** 2 if out_kind == 'power' else np.abs(ref)
+    plan = plan_for(n, freqs, 'float32', 2, kind='morlet', params=(7.0, 0.0))
+    got = plan.execute(x, out_kind=out_kind)
+    assert max_err(got, ref) <= (2e-5 if out_kind == 'power' else 1e-5)
+
+
+@pytest.mark.parametrize('dtype', ['float32', 'float64'])
+def test_interpolate_at_n16384(dtype):
+    """interpolate=True (base.py:107-123: the wavelet and X above int(N/2) zeroed) at C4's
+    length through the drop-in class, against the oracle."""
+    n, freqs = 16384, np.array([1., 17., 90., 256., 400.])
+    x = synth(1, n, seed=5)[0].astype(np.float64)
+    ref = O.cwt('morse', x, freqs, interpolate=True)
+    got = nw.Morse(1000, interpolate=True, dtype=dtype).cwt(x.astype(dtype), freqs)
+    assert max_err(got, ref) <= (1e-12 if dtype == 'float64' else 1e-5)
