@@ -83,6 +83,24 @@ __device__ __forceinline__ C2<T> chirp(int k, uint32_t n2, float inv_n2, const C
     }
 }
 
+// fp32 chirp from an exact phase index m = k^2 mod 2n (revolutions m / 2n)
+__device__ __forceinline__ C2<float> chirp_m(uint32_t m, float inv_n2) {
+    const float rev = (float)m * inv_n2;
+    return C2<float>{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
+}
+// (a + b) mod n for a, b < n: one add, one subtract, one unsigned min
+__device__ __forceinline__ uint32_t addmod(uint32_t a, uint32_t b, uint32_t n) {
+    const uint32_t s = a + b;
+    return min(s, s - n);
+}
+#ifndef NW_CHIRP_INC
+#define NW_CHIRP_INC 0   // fp32 phase indices k^2 mod 2n by exact modular increments instead of a urem
+                         // per element: measured 2.7 % slower (n = 1201 power and cwt), off
+#endif
+#ifndef NW_CHIRP_SKIP_EPI
+#define NW_CHIRP_SKIP_EPI 1   // |y| and |y|^2 skip the final chirp: |c(n) y'| = |y'|
+#endif
+
 template <typename T, bool REALW> struct WRow;
 template <typename T> struct WRow<T, true> {
     using type = T;
@@ -131,6 +149,11 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     const float inv_n2 = 1.0f / (float)n2;
     const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * n;
     const int nz = (ksup[fi] + TT - 1) / TT;   // pass-0 elements reaching the support (<= E/2)
+    // fp32 phase index of k = t + r*T: m_r = k^2 mod 2n, m_{r+1} = m_r + s_r, s_r = (2 T k + T^2)
+    // mod 2n, s_{r+1} = s_r + 2 T^2 (all mod 2n; exact, t < T <= 1024)
+    const uint32_t mk0 = ((uint32_t)t * (uint32_t)t) % n2;
+    const uint32_t sk0 = (2u * TT * (uint32_t)t + (uint32_t)TT * TT) % n2;
+    const uint32_t dk = (2u * TT * TT) % n2;
     Tab1<T, M, E>::fill(lds, tw, t);
     for (int64_t s = s_begin; s < s_end; ++s) {
         const cplx<T>* Xs = X + s * d.nh;
@@ -139,15 +162,22 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
         // only the elements r < NZ (bins k < NZ*T) can meet the row's support K <= M/2: the
         // others are zero for every thread and the DIF stages skip them (as nw_fused's pass 0)
         auto pass0 = [&]<int NZ>() {
+            uint32_t mk = mk0, sk = sk0;
+            asm volatile("" : "+v"(mk), "+v"(sk));   // per row: not hoisted as NZ live values
 #pragma unroll
             for (int r = 0; r < E; ++r) {
                 const int k = t + r * TT;
                 C2<T> a{T(0), T(0)};
                 if (r < NZ && k < n) {
                     const C2<T> z = WRow<T, REALW>::apply(wrow[k], spectrum_bin<T>(Xs, d, k));
-                    a = cmul(z, chirp<T>(k, n2, inv_n2, ct));
+                    if constexpr (sizeof(T) == 4 && NW_CHIRP_INC) a = cmul(z, chirp_m(mk, inv_n2));
+                    else a = cmul(z, chirp<T>(k, n2, inv_n2, ct));
                 }
                 v[r] = C2<T>{a.re, -a.im};
+                if (r + 1 < NZ) {
+                    mk = addmod(mk, sk, n2);
+                    sk = addmod(sk, dk, n2);
+                }
             }
             idft_br<T, E, NZ>(v);
         };
@@ -176,15 +206,38 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
         lds_read<T, M, E, 1, 1, kRegOsz>(v, lds, t);
         idft_br<T, E>(v);
         passes_regs<T, M, E, 1>(v, lds, t, tw);
-        // y[n] = c(n) y'[n] for n < N
+        // y[n] = c(n) y'[n] for n < N (|y|, |y|^2: |c(n)| = 1, the chirp is skipped)
         O* orow = reinterpret_cast<O*>(out) + (s * d.nfreq + fi) * (int64_t)n;
 #pragma unroll
-        for (int q = 0; q < IL::Q; ++q)
-#pragma unroll
-            for (int i = 0; i < IL::R; ++i) {
-                const int idx = t + q * TT + bitrev<IL::R>(i) * IL::NS;
-                if (idx < n) orow[idx] = out_value<OUT, T>(cmul(v[q * IL::R + i], chirp<T>(idx, n2, inv_n2, ct)));
+        for (int q = 0; q < IL::Q; ++q) {
+            // outputs n_j = n0 + j*NS in natural j order (register i = bitrev(j)); fp32 phase
+            // indices by modular increments from n0^2 mod 2n
+            const uint32_t n0 = (uint32_t)(t + q * TT);
+            uint32_t mn = 0, sn = 0, dn = 0;
+            constexpr bool EPI = OUT == NW_OUT_CWT || !NW_CHIRP_SKIP_EPI;
+            if constexpr (EPI && sizeof(T) == 4 && NW_CHIRP_INC) {
+                mn = (n0 * n0) % n2;
+                sn = (2u * n0 * (uint32_t)IL::NS + (uint32_t)IL::NS * IL::NS) % n2;
+                dn = (2u * (uint32_t)IL::NS * IL::NS) % n2;
             }
+#pragma unroll
+            for (int j = 0; j < IL::R; ++j) {
+                const int i = bitrev<IL::R>(j);
+                const int idx = (int)n0 + j * IL::NS;
+                C2<T> y = v[q * IL::R + i];
+                if constexpr (EPI) {
+                    if constexpr (sizeof(T) == 4 && NW_CHIRP_INC) y = cmul(y, chirp_m(mn, inv_n2));
+                    else y = cmul(y, chirp<T>(idx, n2, inv_n2, ct));
+                }
+                if (idx < n) orow[idx] = out_value<OUT, T>(y);
+                if constexpr (EPI && sizeof(T) == 4 && NW_CHIRP_INC) {
+                    if (j + 1 < IL::R) {
+                        mn = addmod(mn, sn, n2);
+                        sn = addmod(sn, dn, n2);
+                    }
+                }
+            }
+        }
     }
 }
 
