@@ -654,8 +654,11 @@ struct LastStores {
 #ifndef NW_XDMA64
 #define NW_XDMA64 1   // fp64 E = 32 too: n = 16384 fp64 cwt 10.90 -> 9.88 ms per 512-signal launch (one box)
 #endif
+#ifndef NW_XDMA64_MIN_E
+#define NW_XDMA64_MIN_E 32
+#endif
 template <typename T, int E, bool REALW>
-constexpr bool kXDMA = (sizeof(T) == 4 || NW_XDMA64) && E >= NW_XDMA_MIN_E && REALW;
+constexpr bool kXDMA = (sizeof(T) == 4 ? E >= NW_XDMA_MIN_E : (NW_XDMA64 && E >= NW_XDMA64_MIN_E)) && REALW;
 // DMA rounds (T lanes x 16 B each) holding the first nz pass-0 elements (T bins each)
 template <typename T> __device__ __forceinline__ int dma_rounds_for(int nz) {
     return (nz * (int)sizeof(C2<T>) + 15) / 16;
