@@ -297,18 +297,30 @@ int chirp_table(nw_plan* p) {
     return NW_OK;
 }
 
+#ifndef NW_OWN_FORWARD
+#define NW_OWN_FORWARD 1   // fused sizes: forward R2C by nw_fused.hip's fwd_r2c_kernel (no copy, one kernel)
+#endif
+
 int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
-    // rocFFT may use its input as scratch: transform from the plan's own copy.
-    if (xs_dev != p->d_x)
-        NW_TRY(staged(p, ST_COPY, [&] {
-            NW_HIP(hipMemcpyAsync(p->d_x, xs_dev, (size_t)c * p->n * p->esz, hipMemcpyDeviceToDevice, p->stream));
+    if (NW_OWN_FORWARD && !rocfft_engine && !p->large && !p->chirp) {
+        // power-of-two n <= 16384: the on-chip forward transform reads the caller's rows directly
+        NW_TRY(staged(p, ST_FWD, [&] {
+            NW_HIP(nw::fused_forward(p->n, p->dtype, xs_dev, p->d_X, c, p->nh, p->stream));
             return NW_OK;
         }));
-    NW_TRY(staged(p, ST_FWD, [&] {
-        return run_fft_rows(p, false, c, (char*)p->d_x, (char*)p->d_X, (size_t)p->n * p->esz,
-                            (size_t)p->nh * 2 * p->esz);
-    }));
+    } else {
+        // rocFFT may use its input as scratch: transform from the plan's own copy.
+        if (xs_dev != p->d_x)
+            NW_TRY(staged(p, ST_COPY, [&] {
+                NW_HIP(hipMemcpyAsync(p->d_x, xs_dev, (size_t)c * p->n * p->esz, hipMemcpyDeviceToDevice, p->stream));
+                return NW_OK;
+            }));
+        NW_TRY(staged(p, ST_FWD, [&] {
+            return run_fft_rows(p, false, c, (char*)p->d_x, (char*)p->d_X, (size_t)p->n * p->esz,
+                                (size_t)p->nh * 2 * p->esz);
+        }));
+    }
 
     if (!rocfft_engine && p->large) {
         // two-pass form (n > 16384): per signal, X -> Xt, then per chunk of scales the

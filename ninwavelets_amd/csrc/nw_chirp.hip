@@ -84,12 +84,12 @@ __device__ __forceinline__ C2<T> chirp(int k, uint32_t n2, float inv_n2, const C
 }
 
 // fp32 chirp from an exact phase index m = k^2 mod 2n (revolutions m / 2n)
-__device__ __forceinline__ C2<float> chirp_m(uint32_t m, float inv_n2) {
+[[maybe_unused]] __device__ __forceinline__ C2<float> chirp_m(uint32_t m, float inv_n2) {
     const float rev = (float)m * inv_n2;
     return C2<float>{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
 }
 // (a + b) mod n for a, b < n: one add, one subtract, one unsigned min
-__device__ __forceinline__ uint32_t addmod(uint32_t a, uint32_t b, uint32_t n) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t addmod(uint32_t a, uint32_t b, uint32_t n) {
     const uint32_t s = a + b;
     return min(s, s - n);
 }

@@ -269,6 +269,11 @@ template <typename T, int N, int E> constexpr int kImgElems = kPad16<T, N, E> ? 
 // output value of one point: y, |y| or |y|^2
 template <int OUT, typename T> struct OutT { using type = T; };
 template <typename T> struct OutT<NW_OUT_CWT, T> { using type = C2<T>; };
+// internal output kind of the forward R2C kernel (fused_forward): conj(y[k]) for k <= n/2,
+// stored lane-contiguous (a 16-B "output" size keeps the last pass unpaired)
+constexpr int kOutXHalf = 1000;
+struct alignas(16) XHalfSlot { double a, b; };
+template <typename T> struct OutT<kOutXHalf, T> { using type = XHalfSlot; };
 template <int OUT, typename T>
 __device__ __forceinline__ typename OutT<OUT, T>::type out_value(C2<T> y) {
     if constexpr (OUT == NW_OUT_CWT) return y;
@@ -794,7 +799,18 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
             }
         }
         NW_STAMP(st, 2 * P);                   // pass P arithmetic
-        if constexpr (I::LAST) {
+        if constexpr (I::LAST && OUT == kOutXHalf) {
+            // forward R2C: X[k] = conj(sum_n x[n] w^(+kn)) for k <= n/2 (row stride n/2 + 1)
+            static_assert(!I::PAIRED, "forward stores are lane-contiguous");
+            C2<S>* xr = reinterpret_cast<C2<S>*>(ocur);
+#pragma unroll
+            for (int q = 0; q < Q; ++q)
+#pragma unroll
+                for (int i = 0; i < R; ++i) {
+                    const int k = I::bfly(t, q) + bitrev<R>(i) * I::NS;
+                    if (k <= N / 2) xr[k] = C2<S>{v[q * R + i].re, -v[q * R + i].im};
+                }
+        } else if constexpr (I::LAST) {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (PAIRSIG) {
                 C2<S> a[E], b[E];

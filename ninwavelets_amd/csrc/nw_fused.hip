@@ -389,6 +389,30 @@ __global__ __launch_bounds__(N / E, NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc
     }
 }
 
+// Forward R2C of the signals for the fused engine (replaces rocFFT's two-kernel R2C and the
+// copy it needs, since rocFFT may use its input as scratch): one block per signal, the same
+// pass machinery on v[r] = x[t + r*T] (imaginary parts zero), X[k] = conj(y[k]) for k <= n/2
+// (scipy/rocFFT's unnormalised forward transform, base.py:399).
+template <typename T, int N, int E>
+__global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void fwd_r2c_kernel(const T* __restrict__ x,
+                                                                              C2<T>* __restrict__ X,
+                                                                              const C2<T>* __restrict__ tw,
+                                                                              int64_t nh) {
+    using G = Geometry<N, E>;
+    extern __shared__ __align__(16) unsigned char smem[];
+    T* lds = reinterpret_cast<T*>(smem);
+    const int t = threadIdx.x;
+    const int64_t s = blockIdx.x;
+    Tab1<T, N, E>::fill(lds, tw, t);
+    const T* xs = x + s * (int64_t)N;
+    const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(T);
+    C2<T> v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) v[r] = C2<T>{*at(xs, xo, (uint32_t)(r * G::T * sizeof(T))), T(0)};
+    idft_br<T, E>(v);
+    passes_from<T, N, E, kOutXHalf, 1, false>(v, lds, t, tw, nullptr, nullptr, X + s * nh, nullptr);
+}
+
 // W[f, k] for the fused engine: the reference's cached row, pad_to'd to n, 1/n folded
 // in (real rows for analytic kinds, complex for tables).  Built once per plan+wavelet.
 template <typename T, bool REALW>
@@ -483,6 +507,20 @@ hipError_t twiddles_for(int64_t n, int dtype, void** out) {
     return hipSuccess;
 }
 
+
+template <typename T, int N, int E>
+hipError_t launch_forward(const void* x, void* X, int64_t nsig, int64_t nh, hipStream_t s) {
+    void* tw = nullptr;
+    hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
+    if (e != hipSuccess) return e;
+    const int lds = kLdsBytes<T, N, E>;
+    e = hipFuncSetAttribute((const void*)fwd_r2c_kernel<T, N, E>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+    if (e != hipSuccess) return e;
+    if (nsig > 0x7fffffff) return hipErrorInvalidConfiguration;
+    fwd_r2c_kernel<T, N, E><<<(unsigned)nsig, N / E, lds, s>>>(reinterpret_cast<const T*>(x), reinterpret_cast<C2<T>*>(X),
+                                                             reinterpret_cast<const C2<T>*>(tw), nh);
+    return hipGetLastError();
+}
 
 // bytes of the W rows in the table buffer (the wnz[nfreq] support array follows them)
 size_t wtab_row_bytes(int64_t n, int nfreq, size_t esz, bool realw) {
@@ -640,6 +678,14 @@ hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
         else wsupport_kernel<double, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
     }
     return hipGetLastError();
+}
+
+hipError_t fused_forward(int64_t n, int dtype, const void* x, void* X, int64_t nsig, int64_t nh, hipStream_t s) {
+#define NW_FWD(TY, NN, EE) \
+    if (n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) return launch_forward<TY, NN, EE>(x, X, nsig, nh, s);
+    NW_FUSED_TABLE(NW_FWD)
+#undef NW_FWD
+    return hipErrorNotSupported;
 }
 
 int fused_kernel_id(int64_t n, int dtype, int kind) {

@@ -172,6 +172,8 @@ hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s);
 hipError_t launch_fused(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
                         int64_t nsig, hipStream_t s);
 int        fused_kernel_id(int64_t n, int dtype, int kind);   // NW_K_FUSED or NW_K_FUSED_PAIR
+// forward R2C of nsig real rows of length n (fused sizes) into half spectra of row stride nh
+hipError_t fused_forward(int64_t n, int dtype, const void* x, void* X, int64_t nsig, int64_t nh, hipStream_t s);
 hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 pi i j / n), cached per device
 
 // chirp-z engine (nw_chirp.hip): n not taken by the power-of-two kernels, 2n - 1 <= 16384
