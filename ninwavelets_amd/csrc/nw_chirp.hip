@@ -114,7 +114,11 @@ template <typename T> struct WRow<T, false> {
 // waves per SIMD without scratch (tools/regs.py): fp32 M <= 4096 fit 168 VGPRs (3 waves;
 // 4 spilled 44 B at M = 1024), M >= 8192 and fp64 need up to 256 (2 waves; fp32 M = 16384
 // at E = 32 still spills ~230 B there)
-template <typename T, int M, int E> constexpr int kChirpWps = E <= 8 ? 4 : (sizeof(T) == 4 && M <= 4096) ? 3 : 2;
+#ifndef NW_CHIRP_WPS8192
+#define NW_CHIRP_WPS8192 2
+#endif
+template <typename T, int M, int E>
+constexpr int kChirpWps = E <= 8 ? 4 : (sizeof(T) == 4 && M <= 4096 && E <= 16) ? 3 : (sizeof(T) == 4 && M == 8192 && E <= 16) ? NW_CHIRP_WPS8192 : 2;
 template <typename T, int M, int E, int OUT, bool REALW>
 __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     WDesc d, const cplx<T>* __restrict__ X, const void* __restrict__ wtab, void* __restrict__ out,
@@ -363,8 +367,8 @@ hipError_t chirp_tables(int64_t n, int64_t m, int dtype, void** out) {
 }
 
 template <typename T, int M, int E, bool REALW>
-hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
-                    const int* rowmap, int nrows, const int* ksup, hipStream_t s) {
+hipError_t launch_m_e(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
+                      const int* rowmap, int nrows, const int* ksup, hipStream_t s) {
     constexpr int threads = M / E;
     const int lds = kLdsBytes<T, M, E>;
     void* tw = nullptr;
@@ -395,15 +399,42 @@ hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wta
     return e;
 }
 
+// fp32 M = 8192: |y| and |y|^2 at E = 32 (256 threads, two blocks per CU, 3 passes, no
+// scratch): measured N = 4097 power 10.60 -> 8.75 ms, N = 3001 6.60 -> 5.82 ms per launch;
+// the complex output spills at E = 32 (108-128 B) and keeps E = 16
+#ifndef NW_CHIRP_E8192_POW
+#define NW_CHIRP_E8192_POW 32
+#endif
+#ifndef NW_CHIRP_E4096_POW
+#define NW_CHIRP_E4096_POW 16
+#endif
+#ifndef NW_CHIRP_E2048_POW
+#define NW_CHIRP_E2048_POW 16
+#endif
+template <typename T, int M, int E, bool REALW>
+hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
+                    const int* rowmap, int nrows, const int* ksup, hipStream_t s) {
+    constexpr int EP = sizeof(T) != 4 ? E : M == 8192 ? NW_CHIRP_E8192_POW : M == 4096 ? NW_CHIRP_E4096_POW
+                                            : M == 2048 ? NW_CHIRP_E2048_POW : E;
+    if constexpr (EP != E) {
+        if (out_kind != NW_OUT_CWT)
+            return launch_m_e<T, M, EP, REALW>(d, out_kind, X, wtab, out, nsig, rowmap, nrows, ksup, s);
+    }
+    return launch_m_e<T, M, E, REALW>(d, out_kind, X, wtab, out, nsig, rowmap, nrows, ksup, s);
+}
+
 }  // namespace
 
 // (dtype, M, E) of the chirp engine: fp32 M <= 16384 (E = 32 at 16384), fp64 M <= 8192
 #ifndef NW_CHIRP_E
 #define NW_CHIRP_E 16   // elements per thread, fp32 M <= 8192
 #endif
+#ifndef NW_CHIRP_E8192
+#define NW_CHIRP_E8192 NW_CHIRP_E
+#endif
 #define NW_CHIRP_TABLE(X)                                                                        \
     X(float, 1024, NW_CHIRP_E) X(float, 2048, NW_CHIRP_E) X(float, 4096, NW_CHIRP_E)             \
-    X(float, 8192, NW_CHIRP_E) X(float, 16384, 32)                                               \
+    X(float, 8192, NW_CHIRP_E8192) X(float, 16384, 32)                                           \
     X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) X(double, 8192, 16)
 
 int64_t chirp_mmax(int dtype) { return dtype == NW_F32 ? 16384 : 8192; }
