@@ -125,6 +125,14 @@ struct nw_plan {
     int64_t chirp_counts[5] = {0, 0, 0, 0, 0};   // rows per M class (M = 1024 << c)
     bool chirp_tentative = false;    // auto engine, 2n - 1 > M_max: chirp-z only if every row's
                                      // support fits (checked when the table is built), else rocFFT
+    // chirp-z rows of a tentative length wider than the largest on-chip transform: computed
+    // by the rocFFT path on a compacted view of just those rows (over_desc) into d_oscr and
+    // scattered to their scales (k_expand_rows), the other rows stay on chip
+    std::vector<int> chirp_over;
+    nw::WDesc over_desc{};
+    void* d_obuf = nullptr;          // idx[U], offs[U + 1], order[U], then over_desc's per-row arrays
+    void* d_oscr = nullptr;
+    size_t d_oscr_bytes = 0;
     void* d_scratch = nullptr;       // two-pass form: Xt + B
     size_t d_scratch_bytes = 0;
 
@@ -280,21 +288,121 @@ int run_fft_rows(nw_plan* p, bool inverse, int64_t rows, char* in, char* out, si
 // The chirp-z table (W rows, supports, rows grouped by M) of the current wavelet.  A
 // tentative length (2n - 1 > M_max) whose rows do not all fit switches the plan to the
 // rocFFT engine until the next nw_plan_set_wavelet.
+#ifndef NW_CHIRP_HYBRID
+#define NW_CHIRP_HYBRID 1   // wide rows of a tentative length to rocFFT, the rest on chip
+#endif
+
+// The compacted view of the rows `rows` of the current desc (device arrays gathered on the
+// device): per-row freq / peak / xstep32 / row_len and table rows, plus the scatter map
+// (offs = 0 .. U, order = rows) for k_expand_rows.
+int build_overflow_view(nw_plan* p, const std::vector<int>& rows) {
+    const int U = (int)rows.size();
+    const nw::WDesc& d = p->desc;
+    const bool table = d.kind == NW_TABLE;
+    const size_t trow = table ? (size_t)d.len_full * 2 * p->esz : 0;
+    const size_t o_offs = ((size_t)U * 4 + 15) / 16 * 16, o_order = o_offs + ((size_t)(U + 1) * 4 + 15) / 16 * 16,
+                 o_freq = o_order + ((size_t)U * 4 + 15) / 16 * 16, o_peak = o_freq + (size_t)U * 8,
+                 o_x = o_peak + (size_t)U * 8, o_rl = (o_x + (size_t)U * 4 + 15) / 16 * 16,
+                 o_tab = (o_rl + (size_t)U * 8 + 255) / 256 * 256, bytes = o_tab + (size_t)U * trow;
+    if (p->d_obuf) NW_HIP(hipFree(p->d_obuf));
+    p->d_obuf = nullptr;
+    char* b = nullptr;
+    NW_HIP(hipMalloc((void**)&b, bytes));
+    p->d_obuf = b;
+    std::vector<int32_t> head(o_freq / 4, 0);
+    for (int u = 0; u < U; ++u) {
+        head[u] = rows[u];
+        head[o_offs / 4 + u] = u;
+        head[o_order / 4 + u] = rows[u];
+    }
+    head[o_offs / 4 + U] = U;
+    NW_HIP(hipMemcpy(b, head.data(), o_freq, hipMemcpyHostToDevice));
+    const int32_t* idx = (const int32_t*)b;
+    nw::WDesc o = d;
+    o.nfreq = U;
+    if (d.freq) {
+        NW_HIP(nw::launch_gather(d.freq, b + o_freq, idx, U, 8, p->stream));
+        o.freq = (const double*)(b + o_freq);
+    }
+    if (d.peak) {
+        NW_HIP(nw::launch_gather(d.peak, b + o_peak, idx, U, 8, p->stream));
+        o.peak = (const double*)(b + o_peak);
+    }
+    if (d.xstep32) {
+        NW_HIP(nw::launch_gather(d.xstep32, b + o_x, idx, U, 4, p->stream));
+        o.xstep32 = (const float*)(b + o_x);
+    }
+    if (table && d.row_len) {
+        NW_HIP(nw::launch_gather(d.row_len, b + o_rl, idx, U, 8, p->stream));
+        o.row_len = (const int64_t*)(b + o_rl);
+    }
+    if (table && trow) {
+        NW_HIP(nw::launch_gather(d.table, b + o_tab, idx, U, trow, p->stream));
+        o.table = b + o_tab;
+    }
+    NW_HIP(hipStreamSynchronize(p->stream));
+    p->over_desc = o;
+    p->chirp_over = rows;
+    return NW_OK;
+}
+
 int chirp_table(nw_plan* p) {
     if (p->wtab_valid) return NW_OK;
     NW_TRY(ensure(&p->d_wtab, &p->d_wtab_bytes, nw::chirp_wtable_bytes(p->n, p->nfreq, p->dtype, p->desc.kind)));
     bool fits = true;
-    NW_HIP(nw::build_chirp_wtable(p->desc, p->dtype, p->d_wtab, p->stream, p->chirp_counts, &fits));
+    std::vector<int> over;
+    p->chirp_over.clear();
+    NW_HIP(nw::build_chirp_wtable(p->desc, p->dtype, p->d_wtab, p->stream, p->chirp_counts, &fits, &over));
     if (!fits) {
         if (!p->chirp_tentative)
             return fail(NW_E_INVALID, "chirp-z form: a wavelet row is wider than the largest on-chip transform");
-        p->chirp = false;
-        p->engine = NW_ENGINE_ROCFFT;
-        p->stats.engine = NW_ENGINE_ROCFFT;
-        return NW_OK;
+        if (!NW_CHIRP_HYBRID || (int)over.size() >= p->nfreq) {   // no row fits: the rocFFT engine
+            p->chirp = false;
+            p->engine = NW_ENGINE_ROCFFT;
+            p->stats.engine = NW_ENGINE_ROCFFT;
+            return NW_OK;
+        }
+        NW_TRY(build_overflow_view(p, over));
     }
     p->wtab_valid = true;
     return NW_OK;
+}
+
+// The overflow rows of a hybrid chirp-z plan through the rocFFT path (K1 on the compacted
+// view, in-place C2C inverse, epilogue), then scattered to their scales of dst.
+int run_overflow_rows(nw_plan* p, int64_t c, void* dst, int out_kind) {
+    const int U = (int)p->chirp_over.size();
+    nw::WDesc od = p->over_desc;
+    od.n = p->desc.n;
+    od.nh = p->desc.nh;
+    od.scale = p->desc.scale;
+    od.off = p->desc.off;
+    od.xlim = p->desc.xlim;
+    const size_t crow = (size_t)p->n * 2 * p->esz;
+    const size_t orow = (size_t)p->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
+    const size_t ybytes = (size_t)c * U * crow;
+    NW_TRY(ensure(&p->d_oscr, &p->d_oscr_bytes, ybytes + (out_kind == NW_OUT_CWT ? 0 : (size_t)c * U * orow)));
+    char* Y = (char*)p->d_oscr;
+    NW_TRY(staged(p, ST_MUL, [&] {
+        NW_HIP(nw::launch_multiply(od, p->dtype, p->d_X, Y, c, p->stream));
+        return NW_OK;
+    }));
+    NW_TRY(staged(p, ST_INV, [&] { return run_fft_rows(p, true, c * U, Y, nullptr, crow, crow); }));
+    const char* src = Y;
+    if (out_kind != NW_OUT_CWT) {
+        char* Z = Y + ybytes;
+        NW_TRY(staged(p, ST_EPI, [&] {
+            NW_HIP(nw::launch_epilogue(p->dtype, out_kind, Y, Z, c * U * p->n, p->stream));
+            return NW_OK;
+        }));
+        src = Z;
+    }
+    const int32_t* hb = (const int32_t*)p->d_obuf;
+    const size_t o_offs = ((size_t)U * 4 + 15) / 16 * 16, o_order = o_offs + ((size_t)(U + 1) * 4 + 15) / 16 * 16;
+    return staged(p, ST_EXPAND, [&] {
+        NW_HIP(nw::launch_expand_rows(src, dst, c, U, p->nfreq, orow, hb + o_offs / 4, hb + o_order / 4, p->stream));
+        return NW_OK;
+    });
 }
 
 #ifndef NW_OWN_FORWARD
@@ -360,13 +468,16 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
         // chirp-z form (any other n up to 8192 fp32 / 4096 fp64): two on-chip FFTs per row
         NW_TRY(chirp_table(p));
         p->stats.kernel = NW_K_CHIRP;
-        if (p->chirp)
-            return staged(p, ST_FUSED, [&] {
+        if (p->chirp) {
+            NW_TRY(staged(p, ST_FUSED, [&] {
                 NW_HIP(nw::launch_chirp(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->chirp_counts,
                                         p->stream));
                 return NW_OK;
-            });
-        rocfft_engine = true;   // a tentative length whose rows do not fit: the rocFFT engine
+            }));
+            if (!p->chirp_over.empty()) NW_TRY(run_overflow_rows(p, c, dst, out_kind));
+            return NW_OK;
+        }
+        rocfft_engine = true;   // a tentative length none of whose rows fit: the rocFFT engine
     }
     if (!rocfft_engine) {
         if (!p->wtab_valid) {
@@ -548,7 +659,7 @@ void free_plan(nw_plan* p) {
     if (p->info) rocfft_execution_info_destroy(p->info);
     void* bufs[] = {p->work,   p->d_x,    p->d_X,        p->d_Y,     p->d_out,      p->d_wtab,
                     p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len, p->d_acc, p->d_scratch,
-                    p->d_ubuf, p->d_rep,  p->d_uout};
+                    p->d_ubuf, p->d_rep,  p->d_uout, p->d_obuf, p->d_oscr};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& pe : p->pending) {

@@ -459,7 +459,8 @@ size_t chirp_wtable_bytes(int64_t n, int nfreq, int dtype, int kind) {
     return chirp_w_bytes(n, nfreq, dtype, kind) + 2 * (size_t)nfreq * sizeof(int);
 }
 
-hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts, bool* fits) {
+hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts, bool* fits,
+                              std::vector<int>* overflow) {
     dim3 grid((unsigned)((d.n + 255) / 256), (unsigned)d.nfreq);
     const bool realw = d.kind != NW_TABLE;
     int* ksup = reinterpret_cast<int*>(reinterpret_cast<char*>(wtab) + chirp_w_bytes(d.n, d.nfreq, dtype, d.kind));
@@ -486,9 +487,16 @@ hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t
     std::vector<int> cls(d.nfreq);
     for (int c = 0; c < kChirpClasses; ++c) counts[c] = 0;
     *fits = true;
+    if (overflow) overflow->clear();
     for (int f = 0; f < d.nfreq; ++f) {
         const int64_t need = std::max<int64_t>(d.n + std::max(ks[f], 1) - 1, 2 * (int64_t)ks[f]);
-        if (need > mfull) *fits = false;
+        if (need > mfull) {
+            // wider than the largest on-chip transform: listed for the caller (rocFFT rows)
+            *fits = false;
+            if (overflow) overflow->push_back(f);
+            cls[f] = -1;
+            continue;
+        }
         int64_t m = 1024;
         while (m < need && m < mfull) m <<= 1;
         int c = 0;

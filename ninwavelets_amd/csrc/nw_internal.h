@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <vector>
+
 #include "../../include/ninwave.h"
 #include "nw_host.h"
 
@@ -126,6 +128,7 @@ hipError_t launch_multiply(const WDesc& d, int dtype, const void* X, void* Y, in
 hipError_t launch_epilogue(int dtype, int out_kind, const void* Y, void* out, int64_t count, hipStream_t s);
 hipError_t launch_rows(const WDesc& d, int dtype, void* rows, hipStream_t s);
 // repeated rows: dst (nsig, nf, row) from src (nsig, nu, row), scales grouped by distinct row
+hipError_t launch_gather(const void* src, void* dst, const int32_t* idx, int count, size_t elem_bytes, hipStream_t s);
 hipError_t launch_expand_rows(const void* src, void* dst, int64_t nsig, int nu, int nf, size_t row_bytes,
                               const int32_t* offs, const int32_t* order, hipStream_t s);
 // epoch reductions: source kinds of launch_accumulate
@@ -183,7 +186,10 @@ bool       chirp_possible(int64_t n, int dtype);   // also n < M_max when every 
 size_t     chirp_wtable_bytes(int64_t n, int nfreq, int dtype, int kind);
 // builds W, each row's support and the rows grouped by M class (M = 1024 << c, c < 5:
 // counts[c] rows each; synchronises s once); launch_chirp runs one kernel per class
-hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts, bool* fits);
+// rows whose support does not fit the largest on-chip transform get no M class: *fits is
+// false and (overflow non-null) their indices are listed; counts[] covers the others
+hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s, int64_t* counts, bool* fits,
+                              std::vector<int>* overflow);
 hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
                         int64_t nsig, const int64_t* counts, hipStream_t s);
 

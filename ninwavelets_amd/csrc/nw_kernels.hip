@@ -498,6 +498,26 @@ __global__ __launch_bounds__(256) void k_expand_rows(const V* __restrict__ src, 
     }
 }
 
+// dst[i] = src[idx[i]] for elements of elem_bytes (a multiple of 4): the compacted per-row
+// arrays (and table rows) of a row subset
+__global__ __launch_bounds__(256) void k_gather_elems(const uint32_t* __restrict__ src, uint32_t* __restrict__ dst,
+                                                      const int32_t* __restrict__ idx, int count, int64_t words) {
+    const int64_t total = (int64_t)count * words;
+    for (int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x; g < total; g += (int64_t)gridDim.x * 256) {
+        const int64_t i = g / words, w = g - i * words;
+        dst[g] = src[(int64_t)idx[i] * words + w];
+    }
+}
+
+hipError_t launch_gather(const void* src, void* dst, const int32_t* idx, int count, size_t elem_bytes, hipStream_t s) {
+    if (count <= 0 || elem_bytes == 0) return hipSuccess;
+    if (elem_bytes % 4) return hipErrorInvalidValue;
+    const int64_t words = (int64_t)(elem_bytes / 4);
+    const int64_t blocks = std::min<int64_t>(((int64_t)count * words + 255) / 256, int64_t(1) << 16);
+    k_gather_elems<<<(unsigned)blocks, 256, 0, s>>>((const uint32_t*)src, (uint32_t*)dst, idx, count, words);
+    return hipGetLastError();
+}
+
 hipError_t launch_expand_rows(const void* src, void* dst, int64_t nsig, int nu, int nf, size_t row_bytes,
                               const int32_t* offs, const int32_t* order, hipStream_t s) {
     using V4 = unsigned int __attribute__((ext_vector_type(4)));

@@ -150,10 +150,39 @@ def test_chirp_tentative_lengths(dtype, n):
     wide = np.array([2., 5., 400.])                  # 400 Hz: support ~ n
     g = L.trans_grid(n / 1000., 1000., False)
     p.set_wavelet('morse', [17.5, 3.], wide, g)
-    got = p.execute(x, out_kind='power')
-    assert p.stats()['engine'] == 'rocfft'
-    assert within(got, oracle('morse', x, wide, 'power'), dtype, 'power')
+    for out in ('power', 'cwt', 'abs'):
+        # hybrid: the 2 and 5 Hz rows on chip, the 400 Hz row through the rocFFT path
+        got = p.execute(x, out_kind=out)
+        assert p.stats()['engine'] == 'fused'
+        assert within(got, oracle('morse', x, wide, out), dtype, out), out
+    allwide = np.array([300., 400.])                 # no row fits: the whole wavelet on rocFFT
+    p2 = chirp_plan(n, 2, dtype, 'morse', (17.5, 3.), allwide, max_batch=2)
+    got = p2.execute(x, out_kind='power')
+    assert p2.stats()['engine'] == 'rocfft'
+    assert within(got, oracle('morse', x, allwide, 'power'), dtype, 'power')
     p.set_wavelet('morse', [17.5, 3.], narrow, g)
     got = p.execute(x, out_kind='abs')
     assert p.stats()['engine'] == 'fused'
     assert within(got, oracle('morse', x, narrow, 'abs'), dtype, 'abs')
+
+
+@pytest.mark.parametrize('dtype,n', [('float32', 10001), ('float64', 4097)])
+def test_chirp_hybrid_reductions_and_repeated_rows(dtype, n):
+    """Hybrid rows (some on chip, the wide ones via rocFFT) under the epoch reductions and
+    under repeated rows (the distinct-row view): against the oracle."""
+    S = 5
+    x = synth(S, n, 77).astype(dtype)
+    freqs = np.array([3., 420., 3., 420., 40.])       # repeated: U = 3 > F/2, no dedup view
+    p = chirp_plan(n, len(freqs), dtype, 'morse', (17.5, 3.), freqs, max_batch=2)
+    ref = oracle('morse', x, freqs, 'cwt')
+    pm = p.execute(x, out_kind='power_mean')
+    assert p.stats()['engine'] == 'fused'
+    assert within(pm, np.mean(np.abs(ref) ** 2, axis=0), dtype, 'power')
+    itc = p.execute(x, out_kind='itc')
+    t = 1e-10 if dtype == 'float64' else 1e-3
+    assert np.max(np.abs(itc - np.abs(np.mean(ref / np.abs(ref), axis=0)))) <= t
+    rep = np.array([3., 420., 3., 420.])              # U = 2 <= F/2: the distinct-row view
+    p2 = chirp_plan(n, len(rep), dtype, 'morse', (17.5, 3.), rep, max_batch=2)
+    got = p2.execute(x, out_kind='cwt')
+    assert p2.stats()['unique_rows'] == 2 and p2.stats()['engine'] == 'fused'
+    assert within(got, oracle('morse', x, rep, 'cwt'), dtype, 'cwt')
