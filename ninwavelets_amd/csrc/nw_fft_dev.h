@@ -178,14 +178,19 @@ template <int R> constexpr int ilog2() { return R <= 1 ? 0 : 1 + ilog2<R / 2>();
 // power is a product of at most log2(R) of them: a few ulp, no recurrence drift.
 // The bases are loaded a phase ahead of use (before the LDS exchange that feeds
 // the pass) so the table latency hides under the exchange.
-template <typename T, int R, int N, int NSR>
-__device__ __forceinline__ void twiddle_bases(C2<T>* p, int m, const C2<T>* __restrict__ tw) {
+template <typename T, int R, int N, int NSR, bool SPLIT = false>
+__device__ __forceinline__ void twiddle_bases(C2<T>* p, int m, const C2<T>* __restrict__ tw,
+                                              const C2<T>* split = nullptr) {
     // the twiddles depend on the thread only: keep the compiler from hoisting all of
     // them out of the signal loop (that keeps ~120 values live and spills)
     asm volatile("" : "+v"(m));
 #pragma unroll
     for (int k = 0; k < ilog2<R>(); ++k) {
-        if constexpr (sizeof(T) == 4 && NW_HWTWIDDLE) {
+        if constexpr (SPLIT) {
+            // w_N^i = hi[i >> 5] * lo[i & 31] from the LDS split table (TwSplit), i < N/2
+            const uint32_t i = ((uint32_t)m << k) * (uint32_t)(N / NSR);
+            p[k] = cmul(split[i >> 5], split[N / 64 + (i & 31)]);
+        } else if constexpr (sizeof(T) == 4 && NW_HWTWIDDLE) {
             // v_cos/v_sin take revolutions; (m << k) / NSR is exact in fp32 (power-of-two
             // denominator), measured max abs error 1.2e-7 over all 16384 angles: no memory
             // access, so nothing queues behind this wave's in-flight stores
@@ -685,8 +690,38 @@ template <typename T, int N, int E> struct XBuf {
         return reinterpret_cast<C2<T>*>(reinterpret_cast<char*>(lds) + OFFSET);
     }
 };
+// fp64 twiddle bases from a split table in LDS: w_N^i = hi[i >> 5] * lo[i & 31] for i < N/2,
+// N/64 + 32 exact entries (4.5 KiB at N = 16384) filled once per block from the exact global
+// table, so no base is a global load (a load issued after this wave's stores waits for all
+// of them in the in-order vmcnt queue; fp32 takes v_sin/v_cos for the same reason).  The
+// product of two exact entries is within 1 ulp of a direct entry.
+// Measured (one box, interleaved): fp64 N = 4096 1.950 -> 1.900 ms per launch (+2.7 %), but
+// N = 16384 (E = 32, X by LDS-DMA) 9.80 -> 10.0-10.3 ms and the C5 fp64 row pass 0.94 -> 0.95:
+// on for N <= 4096 only.
+#ifndef NW_TWSPLIT64
+#define NW_TWSPLIT64 1
+#endif
+#ifndef NW_TWSPLIT64_MAXN
+#define NW_TWSPLIT64_MAXN 4096
+#endif
+template <typename T, int N, int E> struct TwSplit {
+    static constexpr bool ON = NW_TWSPLIT64 && std::is_same<T, double>::value && N >= 2048 && N <= NW_TWSPLIT64_MAXN;
+    static constexpr int NHI = N / 64, COUNT = NHI + 32;
+    static constexpr int OFFSET = XBuf<T, N, E>::OFFSET + XBuf<T, N, E>::BYTES;
+    static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<T>) : 0;
+    __device__ static __forceinline__ const C2<T>* table(const T* lds) {
+        return reinterpret_cast<const C2<T>*>(reinterpret_cast<const char*>(lds) + OFFSET);
+    }
+    // call before the first lds_barrier that precedes any use
+    __device__ static __forceinline__ void fill(T* lds, const C2<T>* __restrict__ tw, int t) {
+        if constexpr (ON) {
+            C2<T>* tab = reinterpret_cast<C2<T>*>(reinterpret_cast<char*>(lds) + OFFSET);
+            for (int i = t; i < COUNT; i += Geometry<N, E>::T) tab[i] = i < NHI ? tw[i * 32] : tw[i - NHI];
+        }
+    }
+};
 template <typename T, int N, int E> constexpr int kLdsBytes =
-    kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES + XBuf<T, N, E>::BYTES;
+    kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES + XBuf<T, N, E>::BYTES + TwSplit<T, N, E>::BYTES;
 
 
 // ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P.
@@ -710,17 +745,20 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
     if constexpr (P < Geometry<N, E>::npass()) {
         constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
         constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;
+        constexpr bool SPLIT = TwSplit<T, N, E>::ON;
+        const C2<S>* split = nullptr;
+        if constexpr (SPLIT) split = reinterpret_cast<const C2<S>*>(TwSplit<T, N, E>::table(lds));
         C2<S> pb[Q][LR > 0 ? LR : 1];
 #ifndef NW_ABL_NOTWIDDLE
         if constexpr (!TABLED && I::PAIRED && Q == 2 && NW_TW_PAIR) {
             // the lane's second butterfly is j + 1 (j even, no wrap mod NS): its bases are the
             // first's times the constants w^(2^k) -- uniform loads from the exact table
-            twiddle_bases<S, R, N, I::NS * R>(pb[0], I::bfly(t, 0) % I::NS, tw);
+            twiddle_bases<S, R, N, I::NS * R, SPLIT>(pb[0], I::bfly(t, 0) % I::NS, tw, split);
 #pragma unroll
             for (int k = 0; k < LR; ++k) pb[1][k] = cmul(pb[0][k], tw[(N / (I::NS * R)) << k]);
         } else if constexpr (!TABLED) {
 #pragma unroll
-            for (int q = 0; q < Q; ++q) twiddle_bases<S, R, N, I::NS * R>(pb[q], I::bfly(t, q) % I::NS, tw);
+            for (int q = 0; q < Q; ++q) twiddle_bases<S, R, N, I::NS * R, SPLIT>(pb[q], I::bfly(t, q) % I::NS, tw, split);
         }
 #endif
 #ifndef NW_ABL_NOEXCH

@@ -174,6 +174,8 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     Stamps* st = nullptr;
 #endif
     Tab1<T, N, E>::fill(lds, tw, t);   // read after the first exchange's barriers
+    TwSplit<T, N, E>::fill(lds, tw, t);
+    if constexpr (TwSplit<T, N, E>::ON) lds_barrier();   // read before the first exchange
     C2<T> x[E];
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T));
     // XDMA: X[N/2] (the real Nyquist bin, outside the DMA'd half) of the signal being
@@ -404,6 +406,8 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void fwd_r2c_kernel
     const int t = threadIdx.x;
     const int64_t s = blockIdx.x;
     Tab1<T, N, E>::fill(lds, tw, t);
+    TwSplit<T, N, E>::fill(lds, tw, t);
+    if constexpr (TwSplit<T, N, E>::ON) lds_barrier();
     const T* xs = x + s * (int64_t)N;
     const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(T);
     C2<T> v[E];

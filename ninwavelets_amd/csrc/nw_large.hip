@@ -269,6 +269,8 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_
     if constexpr (KIND != NW_TABLE) wf.init(d, fi);
 
     Tab1<T, N2, E>::fill(lds, tw, t);
+    TwSplit<T, N2, E>::fill(lds, tw, t);
+    if constexpr (TwSplit<T, N2, E>::ON) lds_barrier();   // read before the first exchange
     C2<T> x[E];
     // bins k = k1 + n1*k2 with k2 = t + r*T: elements r >= need are zero for every thread;
     // pass 0 runs the variant NZ = nzv(need) elements
