@@ -409,6 +409,11 @@ int run_overflow_rows(nw_plan* p, int64_t c, void* dst, int out_kind) {
 #define NW_OWN_FORWARD 1   // fused sizes: forward R2C by nw_fused.hip's fwd_r2c_kernel (no copy, one kernel)
 #endif
 
+#ifndef NW_REDUCE_PSUM
+#define NW_REDUCE_PSUM 1   // epoch power sums: fused per-block partials (nw::fused_power_partials)
+#endif
+constexpr int OUT_PSUM = 1001;   // internal run_chunk kind: (ceil(c / 8), F, n) fp64 power partials
+
 int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
     if (NW_OWN_FORWARD && !rocfft_engine && !p->large && !p->chirp) {
@@ -486,6 +491,13 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
             NW_HIP(nw::build_wtable(p->desc, p->dtype, p->d_wtab, p->stream));
             p->wtab_valid = true;
         }
+        if (out_kind == OUT_PSUM) {
+            p->stats.kernel = NW_K_FUSED;
+            return staged(p, ST_FUSED, [&] {
+                NW_HIP(nw::fused_power_partials(p->desc, p->dtype, p->d_X, p->d_wtab, dst, c, p->stream));
+                return NW_OK;
+            });
+        }
         p->stats.kernel = nw::fused_kernel_id(p->n, p->dtype, p->desc.kind);
         return staged(p, ST_FUSED, [&] {
             NW_HIP(nw::launch_fused(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->stream));
@@ -547,14 +559,16 @@ struct UniqueRows {
 // One device chunk: (c, F, n) outputs of kind out_kind into dst (device).
 int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     if (!p->dedup) return run_chunk_rows(p, xs_dev, c, dst, out_kind, dst_is_final);
-    const size_t row = (size_t)p->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
-    NW_TRY(ensure(&p->d_uout, &p->d_uout_bytes, (size_t)c * p->nuniq * row));
+    const bool psum = out_kind == OUT_PSUM;   // fp64 partial rows, one per block of signals
+    const size_t row = (size_t)p->n * (psum ? sizeof(double) : (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz);
+    const int64_t crows = psum ? nw::fused_psum_groups(c) : c;
+    NW_TRY(ensure(&p->d_uout, &p->d_uout_bytes, (size_t)c * p->nuniq * row));   // crows <= c
     {
         UniqueRows u(p);   // d_uout is scratch of the CWT's row size: K1 may write it
         NW_TRY(run_chunk_rows(p, xs_dev, c, p->d_uout, out_kind, true));
     }
     return staged(p, ST_EXPAND, [&] {
-        NW_HIP(nw::launch_expand_rows(p->d_uout, dst, c, p->nuniq, p->nfreq, row, p->d_rep, p->d_rep + p->nuniq + 1,
+        NW_HIP(nw::launch_expand_rows(p->d_uout, dst, crows, p->nuniq, p->nfreq, row, p->d_rep, p->d_rep + p->nuniq + 1,
                                       p->stream));
         return NW_OK;
     });
@@ -575,14 +589,22 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     NW_TRY(ensure(&p->d_acc, &p->d_acc_bytes, acc_bytes));
     NW_HIP(hipMemsetAsync(p->d_acc, 0, acc_bytes, p->stream));
     const bool fused = p->engine == NW_ENGINE_FUSED;
-    const int sig_kind = (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
+    // fp32 power sums at the register-resident fused sizes: the kernel sums |y|^2 over each
+    // block of 8 signals in fp64, the accumulator adds the ceil(c / 8) fp64 partials (the same
+    // fp64 additions of the same fp32 values, regrouped; with the dedup view the
+    // partials of the distinct rows are expanded like any output row)
+    const bool psum = NW_REDUCE_PSUM && fused && !phase && !p->large && !p->chirp &&
+                      nw::fused_psum_supported(p->n, p->dtype, p->desc.kind);
+    const int sig_kind = psum ? OUT_PSUM : (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
     const int src_kind = phase ? nw::ACC_PHASE_Y : (fused ? nw::ACC_POWER_REAL : nw::ACC_POWER_Y);
     void* scratch = nullptr;            // rocFFT engine: run_chunk leaves y in d_Y
     if (!fused) {
         NW_TRY(need_Y(p));
         scratch = p->d_Y;
     } else {
-        NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * fn * (phase ? 2 : 1) * p->esz));
+        size_t sb = (size_t)p->max_batch * fn * (phase ? 2 : 1) * p->esz;
+        if (psum) sb = std::max(sb, (size_t)nw::fused_psum_groups(p->max_batch) * fn * sizeof(double));
+        NW_TRY(ensure(&p->d_out, &p->d_out_bytes, sb));
         scratch = p->d_out;
     }
     for (int64_t s0 = 0; s0 < nsig; s0 += p->max_batch) {
@@ -597,7 +619,9 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
         }
         NW_TRY(run_chunk(p, xs, c, scratch, sig_kind, false));
         NW_TRY(staged(p, ST_EPI, [&] {
-            NW_HIP(nw::launch_accumulate(p->dtype, src_kind, scratch, (double*)p->d_acc, fn, c, p->stream));
+            const int64_t rows = psum ? nw::fused_psum_groups(c) : c;
+            NW_HIP(nw::launch_accumulate(psum ? NW_F64 : p->dtype, src_kind, scratch, (double*)p->d_acc, fn, rows,
+                                         p->stream));
             return NW_OK;
         }));
         p->stats.chunks++;

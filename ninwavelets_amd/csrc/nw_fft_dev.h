@@ -277,6 +277,9 @@ template <typename T> struct OutT<NW_OUT_CWT, T> { using type = C2<T>; };
 // internal output kind of the forward R2C kernel (fused_forward): conj(y[k]) for k <= n/2,
 // stored lane-contiguous (a 16-B "output" size keeps the last pass unpaired)
 constexpr int kOutXHalf = 1000;
+// internal output kind of the fused power partial sums: the last pass adds |y|^2 into the
+// caller's per-thread fp64 accumulators instead of storing (epoch reductions, fused_power_partials)
+constexpr int kOutPSum = 1001;
 struct alignas(16) XHalfSlot { double a, b; };
 template <typename T> struct OutT<kOutXHalf, T> { using type = XHalfSlot; };
 template <int OUT, typename T>
@@ -737,7 +740,7 @@ template <typename T, int N, int E, int OUT, int P, bool XD>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
                                             Stamps* st, void* ocur2 = nullptr, int dma_rounds = 1 << 30,
-                                            const void* xs_next2 = nullptr) {
+                                            const void* xs_next2 = nullptr, double* acc = nullptr) {
     using S = Sc<T>;
     constexpr bool PAIRSIG = !std::is_same<T, S>::value;
     constexpr int OSZ = (int)sizeof(typename OutT<OUT, S>::type);
@@ -837,7 +840,14 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
             }
         }
         NW_STAMP(st, 2 * P);                   // pass P arithmetic
-        if constexpr (I::LAST && OUT == kOutXHalf) {
+        if constexpr (I::LAST && OUT == kOutPSum) {
+            // acc[q*R + i] += |y|^2 of output bfly(t, q) + bitrev(i)*NS (the same positions for
+            // every signal of the block): the power output's value, added in fp64 in signal order
+            // like k_accumulate, so the partials reproduce its sums
+            static_assert(!PAIRSIG, "partial sums run the single-signal kernel");
+#pragma unroll
+            for (int e = 0; e < Q * R; ++e) acc[e] += (double)(v[e].re * v[e].re + v[e].im * v[e].im);
+        } else if constexpr (I::LAST && OUT == kOutXHalf) {
             // forward R2C: X[k] = conj(sum_n x[n] w^(+kn)) for k <= n/2 (row stride n/2 + 1)
             static_assert(!I::PAIRED, "forward stores are lane-contiguous");
             C2<S>* xr = reinterpret_cast<C2<S>*>(ocur);
@@ -863,7 +873,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                 LastStores<T, N, E, OUT>::all(v, ocur, t);
             }
         } else {
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, xs_next2);
+            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, xs_next2, acc);
         }
     }
 }

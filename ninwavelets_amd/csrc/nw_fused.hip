@@ -199,6 +199,13 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     // i.e. NZ/2 rounds of 2*T bins, when it reads no mirrored bin (NZ <= E/2)
     const int nzv = nz < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz;
     const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? dma_rounds_for<T>(nzv) : 1 << 30;
+    // power partial sums (kOutPSum): sum over the block's signals of |y|^2 per output point
+    constexpr bool PSUM = OUT == kOutPSum;
+    double acc[PSUM ? E : 1];
+    if constexpr (PSUM) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = 0.0;
+    }
     for (int64_t s = s_begin; s < s_end; ++s) {
         const C2<T>* xl = nullptr;
         if constexpr (XD || XB) {
@@ -250,7 +257,17 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
         void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
-        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds);
+        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds, nullptr,
+                                         PSUM ? acc : nullptr);
+    }
+    if constexpr (PSUM) {
+        // the block's partial: row (group sg, scale fi) of the (groups, F, N) partial buffer
+        using IL = PassInfo<N, E, G::npass() - 1, (int)sizeof(T)>;
+        double* prow = reinterpret_cast<double*>(out) + ((int64_t)sg * d.nfreq + fi) * (int64_t)N;
+#pragma unroll
+        for (int q = 0; q < IL::Q; ++q)
+#pragma unroll
+            for (int i = 0; i < IL::R; ++i) prow[IL::bfly(t, q) + bitrev<IL::R>(i) * IL::NS] = acc[q * IL::R + i];
     }
     // the last signal's outputs
     NW_STAMP(st, kStampsStore);
@@ -574,6 +591,30 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     return hipGetLastError();
 }
 
+template <typename T, int N, int E>
+hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* partials, int64_t nsig, hipStream_t s) {
+    constexpr int threads = N / E;
+    constexpr int kTileF = kTileFT<T>, kTileG = kTileGT<T>;
+    const int lds = kLdsBytes<T, N, E>;
+    void* tw = nullptr;
+    hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
+    if (e != hipSuccess) return e;
+    e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, kOutPSum, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            lds);
+    if (e != hipSuccess) return e;
+    const int64_t nsg = (nsig + kGroup - 1) / kGroup;
+    const int64_t nsg_pad = (nsg + 8 * kTileG - 1) / (8 * kTileG) * (8 * kTileG);
+    const int64_t nfr = (d.nfreq + kTileF - 1) / kTileF;
+    const int64_t blocks = nsg_pad * nfr * kTileF;
+    if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
+    const int* wnz = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
+                                                  wtab_row_bytes(N, d.nfreq, sizeof(T), true));
+    nw_fused_kernel<T, N, E, kOutPSum, true><<<blocks, threads, lds, s>>>(
+        d, reinterpret_cast<const cplx<T>*>(X), wtab, partials, reinterpret_cast<const C2<T>*>(tw), nsig, kGroup,
+        (int)nsg_pad, wnz);
+    return hipGetLastError();
+}
+
 template <typename T, int N, int E, bool REALW>
 hipError_t prepare_one() {
     if constexpr (kPairMode<T, E, REALW>) {
@@ -682,6 +723,36 @@ hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
         else wsupport_kernel<double, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
     }
     return hipGetLastError();
+}
+
+// epoch power partials: fp32, analytic rows, E <= 16 (W and the accumulators in registers)
+#ifndef NW_FUSED_PSUM
+#define NW_FUSED_PSUM 1
+#endif
+template <typename T, int N, int E>
+constexpr bool kPSumOK = NW_FUSED_PSUM && std::is_same<T, float>::value && E <= 16;
+
+bool fused_psum_supported(int64_t n, int dtype, int kind) {
+    if (kind == NW_TABLE || dtype != NW_F32) return false;
+#define NW_PS(TY, NN, EE) \
+    if (n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) return kPSumOK<TY, NN, EE>;
+    NW_FUSED_TABLE(NW_PS)
+#undef NW_PS
+    return false;
+}
+
+int64_t fused_psum_groups(int64_t nsig) { return (nsig + kGroup - 1) / kGroup; }
+
+hipError_t fused_power_partials(const WDesc& d, int dtype, const void* X, const void* wtab, void* partials,
+                                int64_t nsig, hipStream_t s) {
+#define NW_PSL(TY, NN, EE)                                                                                    \
+    if (d.n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) {                                          \
+        if constexpr (kPSumOK<TY, NN, EE>) return launch_psum<TY, NN, EE>(d, X, wtab, partials, nsig, s);     \
+        return hipErrorNotSupported;                                                                          \
+    }
+    NW_FUSED_TABLE(NW_PSL)
+#undef NW_PSL
+    return hipErrorNotSupported;
 }
 
 hipError_t fused_forward(int64_t n, int dtype, const void* x, void* X, int64_t nsig, int64_t nh, hipStream_t s) {
