@@ -412,7 +412,11 @@ int run_overflow_rows(nw_plan* p, int64_t c, void* dst, int out_kind) {
 #ifndef NW_REDUCE_PSUM
 #define NW_REDUCE_PSUM 1   // epoch power sums: fused per-block partials (nw::fused_power_partials)
 #endif
-constexpr int OUT_PSUM = 1001;   // internal run_chunk kind: (ceil(c / 8), F, n) fp64 power partials
+#ifndef NW_REDUCE_PHSUM
+#define NW_REDUCE_PHSUM 1   // epoch phase sums (ITC): the same with y / |y|
+#endif
+constexpr int OUT_PSUM = 1001;    // internal run_chunk kinds: (ceil(c / 8), F, n) fp64 power partials,
+constexpr int OUT_PHSUM = 1002;   // complex fp64 phase partials (y / |y|)
 
 int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
@@ -491,10 +495,11 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
             NW_HIP(nw::build_wtable(p->desc, p->dtype, p->d_wtab, p->stream));
             p->wtab_valid = true;
         }
-        if (out_kind == OUT_PSUM) {
+        if (out_kind == OUT_PSUM || out_kind == OUT_PHSUM) {
             p->stats.kernel = NW_K_FUSED;
             return staged(p, ST_FUSED, [&] {
-                NW_HIP(nw::fused_power_partials(p->desc, p->dtype, p->d_X, p->d_wtab, dst, c, p->stream));
+                NW_HIP(nw::fused_power_partials(p->desc, p->dtype, out_kind == OUT_PHSUM, p->d_X, p->d_wtab, dst, c,
+                                                p->stream));
                 return NW_OK;
             });
         }
@@ -559,8 +564,9 @@ struct UniqueRows {
 // One device chunk: (c, F, n) outputs of kind out_kind into dst (device).
 int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     if (!p->dedup) return run_chunk_rows(p, xs_dev, c, dst, out_kind, dst_is_final);
-    const bool psum = out_kind == OUT_PSUM;   // fp64 partial rows, one per block of signals
-    const size_t row = (size_t)p->n * (psum ? sizeof(double) : (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz);
+    const bool psum = out_kind == OUT_PSUM || out_kind == OUT_PHSUM;   // fp64 partial rows, one per block of signals
+    const size_t row = psum ? (size_t)p->n * sizeof(double) * (out_kind == OUT_PHSUM ? 2 : 1)
+                            : (size_t)p->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
     const int64_t crows = psum ? nw::fused_psum_groups(c) : c;
     NW_TRY(ensure(&p->d_uout, &p->d_uout_bytes, (size_t)c * p->nuniq * row));   // crows <= c
     {
@@ -589,21 +595,23 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     NW_TRY(ensure(&p->d_acc, &p->d_acc_bytes, acc_bytes));
     NW_HIP(hipMemsetAsync(p->d_acc, 0, acc_bytes, p->stream));
     const bool fused = p->engine == NW_ENGINE_FUSED;
-    // fp32 power sums at the register-resident fused sizes: the kernel sums |y|^2 over each
-    // block of 8 signals in fp64, the accumulator adds the ceil(c / 8) fp64 partials (the same
-    // fp64 additions of the same fp32 values, regrouped; with the dedup view the
-    // partials of the distinct rows are expanded like any output row)
-    const bool psum = NW_REDUCE_PSUM && fused && !phase && !p->large && !p->chirp &&
+    // fp32 reductions at the register-resident fused sizes: the kernel sums |y|^2 (ITC: y / |y|)
+    // over each block of 8 signals in fp64, the accumulator adds the ceil(c / 8) fp64 partials
+    // (the same fp64 additions of the same fp32-derived values, regrouped; with the dedup view
+    // the partials of the distinct rows are expanded like any output row)
+    const bool psum = fused && !p->large && !p->chirp && (phase ? NW_REDUCE_PHSUM : NW_REDUCE_PSUM) &&
                       nw::fused_psum_supported(p->n, p->dtype, p->desc.kind);
-    const int sig_kind = psum ? OUT_PSUM : (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
-    const int src_kind = phase ? nw::ACC_PHASE_Y : (fused ? nw::ACC_POWER_REAL : nw::ACC_POWER_Y);
+    const int sig_kind = psum ? (phase ? OUT_PHSUM : OUT_PSUM) : (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
+    // partials: plain fp64 sums (phase partials as 2 fn reals)
+    const int src_kind = psum ? nw::ACC_POWER_REAL
+                              : phase ? nw::ACC_PHASE_Y : (fused ? nw::ACC_POWER_REAL : nw::ACC_POWER_Y);
     void* scratch = nullptr;            // rocFFT engine: run_chunk leaves y in d_Y
     if (!fused) {
         NW_TRY(need_Y(p));
         scratch = p->d_Y;
     } else {
         size_t sb = (size_t)p->max_batch * fn * (phase ? 2 : 1) * p->esz;
-        if (psum) sb = std::max(sb, (size_t)nw::fused_psum_groups(p->max_batch) * fn * sizeof(double));
+        if (psum) sb = std::max(sb, (size_t)nw::fused_psum_groups(p->max_batch) * fn * (phase ? 2 : 1) * sizeof(double));
         NW_TRY(ensure(&p->d_out, &p->d_out_bytes, sb));
         scratch = p->d_out;
     }
@@ -620,8 +628,8 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
         NW_TRY(run_chunk(p, xs, c, scratch, sig_kind, false));
         NW_TRY(staged(p, ST_EPI, [&] {
             const int64_t rows = psum ? nw::fused_psum_groups(c) : c;
-            NW_HIP(nw::launch_accumulate(psum ? NW_F64 : p->dtype, src_kind, scratch, (double*)p->d_acc, fn, rows,
-                                         p->stream));
+            NW_HIP(nw::launch_accumulate(psum ? NW_F64 : p->dtype, src_kind, scratch, (double*)p->d_acc,
+                                         psum && phase ? 2 * fn : fn, rows, p->stream));
             return NW_OK;
         }));
         p->stats.chunks++;

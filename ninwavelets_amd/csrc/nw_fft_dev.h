@@ -280,6 +280,11 @@ constexpr int kOutXHalf = 1000;
 // internal output kind of the fused power partial sums: the last pass adds |y|^2 into the
 // caller's per-thread fp64 accumulators instead of storing (epoch reductions, fused_power_partials)
 constexpr int kOutPSum = 1001;
+// ... and the phase sums of ITC: acc[2e], acc[2e + 1] += y / |y| in fp64
+constexpr int kOutPhSum = 1002;
+#ifndef NW_PHSUM_RSQ
+#define NW_PHSUM_RSQ 1
+#endif
 struct alignas(16) XHalfSlot { double a, b; };
 template <typename T> struct OutT<kOutXHalf, T> { using type = XHalfSlot; };
 template <int OUT, typename T>
@@ -847,6 +852,18 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
             static_assert(!PAIRSIG, "partial sums run the single-signal kernel");
 #pragma unroll
             for (int e = 0; e < Q * R; ++e) acc[e] += (double)(v[e].re * v[e].re + v[e].im * v[e].im);
+        } else if constexpr (I::LAST && OUT == kOutPhSum) {
+            static_assert(!PAIRSIG, "partial sums run the single-signal kernel");
+#pragma unroll
+            for (int e = 0; e < Q * R; ++e) {
+                // |y|^2 of fp32 parts is exact in fp64 up to one rounding (no overflow), so
+                // rsqrt replaces hypot + two divisions (k_accumulate) to within a few fp64 ulp;
+                // y = 0 gives 0 * inf = NaN like the reference's 0/0 (mneutils.py:68)
+                const double re = (double)v[e].re, im = (double)v[e].im;
+                const double inv = NW_PHSUM_RSQ ? rsqrt(re * re + im * im) : 1.0 / hypot(re, im);
+                acc[2 * e] += re * inv;
+                acc[2 * e + 1] += im * inv;
+            }
         } else if constexpr (I::LAST && OUT == kOutXHalf) {
             // forward R2C: X[k] = conj(sum_n x[n] w^(+kn)) for k <= n/2 (row stride n/2 + 1)
             static_assert(!I::PAIRED, "forward stores are lane-contiguous");

@@ -110,8 +110,12 @@ template <typename T> constexpr int kTileGT = sizeof(T) == 8 ? NW_TILEG64 : NW_T
 #define NW_WPS64 2
 #endif
 #define NW_WAVES_PER_SIMD(T, E) (sizeof(T) == 8 ? NW_WPS64 : (E) >= 32 ? NW_WPS32 : NW_WPS16)
+// the ITC partials hold 2E fp64 accumulators (4E VGPRs) on top: one wave per SIMD fewer
+#ifndef NW_WPS_PHSUM
+#define NW_WPS_PHSUM 3
+#endif
 template <typename T, int N, int E, int OUT, bool REALW>
-__global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
+__global__ __launch_bounds__(N / E, OUT == kOutPhSum ? NW_WPS_PHSUM : NW_WAVES_PER_SIMD(T, E)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
                                                             const void* __restrict__ wtab, void* __restrict__ out,
                                                             const C2<T>* __restrict__ tw, int64_t nsig, int group,
                                                             int nsg_pad, const int* __restrict__ wnz) {
@@ -200,11 +204,13 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     const int nzv = nz < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz;
     const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? dma_rounds_for<T>(nzv) : 1 << 30;
     // power partial sums (kOutPSum): sum over the block's signals of |y|^2 per output point
-    constexpr bool PSUM = OUT == kOutPSum;
-    double acc[PSUM ? E : 1];
+    // (kOutPhSum: the sums of y / |y|, two fp64 values per point)
+    constexpr bool PSUM = OUT == kOutPSum || OUT == kOutPhSum;
+    constexpr int NACC = OUT == kOutPhSum ? 2 : 1;
+    double acc[PSUM ? NACC * E : 1];
     if constexpr (PSUM) {
 #pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] = 0.0;
+        for (int e = 0; e < NACC * E; ++e) acc[e] = 0.0;
     }
     for (int64_t s = s_begin; s < s_end; ++s) {
         const C2<T>* xl = nullptr;
@@ -263,11 +269,18 @@ __global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void nw_fused_kerne
     if constexpr (PSUM) {
         // the block's partial: row (group sg, scale fi) of the (groups, F, N) partial buffer
         using IL = PassInfo<N, E, G::npass() - 1, (int)sizeof(T)>;
-        double* prow = reinterpret_cast<double*>(out) + ((int64_t)sg * d.nfreq + fi) * (int64_t)N;
+        double* prow = reinterpret_cast<double*>(out) + ((int64_t)sg * d.nfreq + fi) * (int64_t)N * NACC;
 #pragma unroll
         for (int q = 0; q < IL::Q; ++q)
 #pragma unroll
-            for (int i = 0; i < IL::R; ++i) prow[IL::bfly(t, q) + bitrev<IL::R>(i) * IL::NS] = acc[q * IL::R + i];
+            for (int i = 0; i < IL::R; ++i) {
+                const int k = IL::bfly(t, q) + bitrev<IL::R>(i) * IL::NS, e = q * IL::R + i;
+                if constexpr (NACC == 1) {
+                    prow[k] = acc[e];
+                } else {
+                    *reinterpret_cast<double2*>(prow + 2 * k) = double2{acc[2 * e], acc[2 * e + 1]};
+                }
+            }
     }
     // the last signal's outputs
     NW_STAMP(st, kStampsStore);
@@ -591,7 +604,7 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     return hipGetLastError();
 }
 
-template <typename T, int N, int E>
+template <typename T, int N, int E, int OUT>
 hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* partials, int64_t nsig, hipStream_t s) {
     constexpr int threads = N / E;
     constexpr int kTileF = kTileFT<T>, kTileG = kTileGT<T>;
@@ -599,7 +612,7 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, kOutPSum, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, OUT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                             lds);
     if (e != hipSuccess) return e;
     const int64_t nsg = (nsig + kGroup - 1) / kGroup;
@@ -609,7 +622,7 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
     if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
     const int* wnz = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
                                                   wtab_row_bytes(N, d.nfreq, sizeof(T), true));
-    nw_fused_kernel<T, N, E, kOutPSum, true><<<blocks, threads, lds, s>>>(
+    nw_fused_kernel<T, N, E, OUT, true><<<blocks, threads, lds, s>>>(
         d, reinterpret_cast<const cplx<T>*>(X), wtab, partials, reinterpret_cast<const C2<T>*>(tw), nsig, kGroup,
         (int)nsg_pad, wnz);
     return hipGetLastError();
@@ -743,11 +756,14 @@ bool fused_psum_supported(int64_t n, int dtype, int kind) {
 
 int64_t fused_psum_groups(int64_t nsig) { return (nsig + kGroup - 1) / kGroup; }
 
-hipError_t fused_power_partials(const WDesc& d, int dtype, const void* X, const void* wtab, void* partials,
-                                int64_t nsig, hipStream_t s) {
+hipError_t fused_power_partials(const WDesc& d, int dtype, bool phase, const void* X, const void* wtab,
+                                void* partials, int64_t nsig, hipStream_t s) {
 #define NW_PSL(TY, NN, EE)                                                                                    \
     if (d.n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) {                                          \
-        if constexpr (kPSumOK<TY, NN, EE>) return launch_psum<TY, NN, EE>(d, X, wtab, partials, nsig, s);     \
+        if constexpr (kPSumOK<TY, NN, EE>) {                                                                  \
+            if (phase) return launch_psum<TY, NN, EE, kOutPhSum>(d, X, wtab, partials, nsig, s);              \
+            return launch_psum<TY, NN, EE, kOutPSum>(d, X, wtab, partials, nsig, s);                          \
+        }                                                                                                     \
         return hipErrorNotSupported;                                                                          \
     }
     NW_FUSED_TABLE(NW_PSL)

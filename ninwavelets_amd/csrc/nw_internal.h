@@ -178,13 +178,14 @@ int        fused_kernel_id(int64_t n, int dtype, int kind);   // NW_K_FUSED or N
 // forward R2C of nsig real rows of length n (fused sizes) into half spectra of row stride nh
 hipError_t fused_forward(int64_t n, int dtype, const void* x, void* X, int64_t nsig, int64_t nh, hipStream_t s);
 hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 pi i j / n), cached per device
-// epoch power partials (fused sizes, fp32 analytic rows, E <= 16): per block of signals the
-// sum of |y|^2 over its signals (fp64, in signal order), one (groups, F, n) fp64 row per
-// (group, scale); groups = fused_psum_groups(nsig)
+// epoch reduction partials (fused sizes, fp32 analytic rows, E <= 16): per block of signals
+// the sum over its signals (fp64, in signal order) of |y|^2, or with phase of y / |y|; one
+// (groups, F, n) row of fp64 (phase: complex fp64) per (group, scale);
+// groups = fused_psum_groups(nsig)
 bool fused_psum_supported(int64_t n, int dtype, int kind);
 int64_t fused_psum_groups(int64_t nsig);
-hipError_t fused_power_partials(const WDesc& d, int dtype, const void* X, const void* wtab, void* partials,
-                                int64_t nsig, hipStream_t s);
+hipError_t fused_power_partials(const WDesc& d, int dtype, bool phase, const void* X, const void* wtab,
+                                void* partials, int64_t nsig, hipStream_t s);
 
 // chirp-z engine (nw_chirp.hip): n not taken by the power-of-two kernels, 2n - 1 <= 16384
 // (fp32) / 8192 (fp64); one (scale, signal) row = two on-chip FFTs of M = 2^ceil(log2(2n-1))

@@ -176,3 +176,31 @@ def test_power_mean_fused_partials(n):
     np.testing.assert_allclose(other.execute(x, out_kind='power_sum'), ps, rtol=1e-13)
     orc = np.abs(np.stack([O.cwt('morse', x[s].astype(np.float64), freqs[::51]) for s in range(S)])) ** 2
     assert max_err(pm[::51], orc.mean(axis=0)) <= 2e-5
+
+
+@pytest.mark.parametrize('n', [1024, 4096])
+def test_itc_fused_partials(n):
+    """ITC (mneutils.py:62-71) at the fused sizes: the kernel sums y / |y| (fp64, k_accumulate's
+    formula) over each block of 8 signals.  Against the reference formula on the same plan's
+    cwt output, which runs on the pair kernel (its own fp32 rounding of y; the phase of a small
+    |y| amplifies it: 1e-5), chunk-size independent (phase_sum 1e-13), against the oracle (within
+    2x the materialised cwt's own ITC error)."""
+    S, freqs = 21, np.arange(1, 257, dtype=np.float64)
+    x = synth(S, n, seed=n + 11)
+    plan = plan_for(n, freqs, 'float32', 8)
+    c = plan.execute(x, out_kind='cwt').astype(np.complex128)
+    itc = plan.execute(x, out_kind='itc')
+    assert L.KERNEL_NAMES[plan.stats()['kernel']] == 'nw_fused_kernel'
+    assert itc.shape == (256, n) and itc.dtype == np.float32
+    assert np.max(np.abs(itc - np.abs(np.mean(c / np.abs(c), axis=0)))) <= 1e-5
+    ph = plan.execute(x, out_kind='phase_sum')
+    assert ph.dtype == np.complex128
+    other = plan_for(n, freqs, 'float32', 3)
+    np.testing.assert_allclose(other.execute(x, out_kind='phase_sum'), ph, rtol=1e-13, atol=1e-13 * S)
+    # against the oracle: the phase of fp32 y is ill-conditioned where |y| is small, so the
+    # bound is the materialised fp32 cwt's own ITC error (x2), and 1e-4 absolute
+    o = np.stack([O.cwt('morse', x[s].astype(np.float64), freqs[::51]) for s in range(S)])
+    ref = np.abs(np.mean(o / np.abs(o), axis=0))
+    err_fused = np.max(np.abs(itc[::51] - ref))
+    err_mat = np.max(np.abs(np.abs(np.mean(c[:, ::51] / np.abs(c[:, ::51]), axis=0)) - ref))
+    assert err_fused <= 2 * err_mat + 1e-6 and err_fused <= 1e-4, (err_fused, err_mat)

@@ -16,9 +16,9 @@ for n in (1024, 2048, 4096):
     om = torch.empty((F, n), device='cuda', dtype=torch.float32)
     op = torch.empty((128, F, n), device='cuda', dtype=torch.float32)
     res = {}
-    for kind in ('power_mean', 'power'):
+    for kind in ('power_mean', 'itc', 'power'):
         def once():
-            if kind == 'power_mean':
+            if kind != 'power':
                 plan.execute(x, om, out_kind=kind)
             else:
                 for s0 in range(0, S, 128):
@@ -30,5 +30,6 @@ for n in (1024, 2048, 4096):
             ts.append(time.perf_counter() - t0)
         res[kind] = min(ts) * 1e3
     pts = S * F * n
-    print('%-8s n=%5d power_mean %.3f ms (%.3e pts/s)  power %.3f ms (%.3e pts/s)' % (
-        tag, n, res['power_mean'], pts / res['power_mean'] * 1e3, res['power'], pts / res['power'] * 1e3), flush=True)
+    print('%-8s n=%5d power_mean %.3f ms (%.3e pts/s)  itc %.3f ms  power %.3f ms (%.3e pts/s)' % (
+        tag, n, res['power_mean'], pts / res['power_mean'] * 1e3, res['itc'], res['power'], pts / res['power'] * 1e3),
+        flush=True)
