@@ -58,6 +58,12 @@ __device__ __forceinline__ C2<float> hi(C2<f2> p) { return {p.re.y, p.im.y}; }
 #define NW_TW_PAIR 1   // paired last pass: second butterfly's twiddle bases from the first's
 #endif
 
+// a rounded product that the compiler may not fuse into a following add
+__device__ __forceinline__ double mul_nocontract(double a, double b) {
+#pragma clang fp contract(off)
+    return a * b;
+}
+
 template <typename T> __device__ __forceinline__ C2<T> cmul(C2<T> a, C2<T> b) {
     return {a.re * b.re - a.im * b.im, a.re * b.im + a.im * b.re};
 }
@@ -861,8 +867,10 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                 // y = 0 gives 0 * inf = NaN like the reference's 0/0 (mneutils.py:68)
                 const double re = (double)v[e].re, im = (double)v[e].im;
                 const double inv = NW_PHSUM_RSQ ? rsqrt(re * re + im * im) : 1.0 / hypot(re, im);
-                acc[2 * e] += re * inv;
-                acc[2 * e + 1] += im * inv;
+                // products rounded before the add (no fma into acc): a partial then adds the
+                // same values whichever block boundaries the chunking draws
+                acc[2 * e] += mul_nocontract(re, inv);
+                acc[2 * e + 1] += mul_nocontract(im, inv);
             }
         } else if constexpr (I::LAST && OUT == kOutXHalf) {
             // forward R2C: X[k] = conj(sum_n x[n] w^(+kn)) for k <= n/2 (row stride n/2 + 1)
