@@ -600,7 +600,7 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     // (the same fp64 additions of the same fp32-derived values, regrouped; with the dedup view
     // the partials of the distinct rows are expanded like any output row)
     const bool psum = fused && !p->large && !p->chirp && (phase ? NW_REDUCE_PHSUM : NW_REDUCE_PSUM) &&
-                      nw::fused_psum_supported(p->n, p->dtype, p->desc.kind);
+                      nw::fused_psum_supported(p->n, p->dtype, p->desc.kind, phase);
     const int sig_kind = psum ? (phase ? OUT_PHSUM : OUT_PSUM) : (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
     // partials: plain fp64 sums (phase partials as 2 fn reals)
     const int src_kind = psum ? nw::ACC_POWER_REAL

@@ -114,8 +114,14 @@ template <typename T> constexpr int kTileGT = sizeof(T) == 8 ? NW_TILEG64 : NW_T
 #ifndef NW_WPS_PHSUM
 #define NW_WPS_PHSUM 3
 #endif
+// ... and the power partials at E = 32 hold E fp64 accumulators on top of a 128-VGPR kernel
+#ifndef NW_WPS_PSUM32
+#define NW_WPS_PSUM32 2
+#endif
+#define NW_WPS_OF(T, E, OUT) \
+    ((OUT) == kOutPhSum ? NW_WPS_PHSUM : ((OUT) == kOutPSum && (E) >= 32) ? NW_WPS_PSUM32 : NW_WAVES_PER_SIMD(T, E))
 template <typename T, int N, int E, int OUT, bool REALW>
-__global__ __launch_bounds__(N / E, OUT == kOutPhSum ? NW_WPS_PHSUM : NW_WAVES_PER_SIMD(T, E)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
+__global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
                                                             const void* __restrict__ wtab, void* __restrict__ out,
                                                             const C2<T>* __restrict__ tw, int64_t nsig, int group,
                                                             int nsg_pad, const int* __restrict__ wnz) {
@@ -742,13 +748,18 @@ hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
 #ifndef NW_FUSED_PSUM
 #define NW_FUSED_PSUM 1
 #endif
+#ifndef NW_PSUM_MAXE
+#define NW_PSUM_MAXE 32   // power partials up to E = 32 (N = 8192, 16384)
+#endif
 template <typename T, int N, int E>
-constexpr bool kPSumOK = NW_FUSED_PSUM && std::is_same<T, float>::value && E <= 16;
+constexpr bool kPSumOK = NW_FUSED_PSUM && std::is_same<T, float>::value && E <= NW_PSUM_MAXE;
+template <typename T, int N, int E>
+constexpr bool kPhSumOK = NW_FUSED_PSUM && std::is_same<T, float>::value && E <= 16;
 
-bool fused_psum_supported(int64_t n, int dtype, int kind) {
+bool fused_psum_supported(int64_t n, int dtype, int kind, bool phase) {
     if (kind == NW_TABLE || dtype != NW_F32) return false;
 #define NW_PS(TY, NN, EE) \
-    if (n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) return kPSumOK<TY, NN, EE>;
+    if (n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) return phase ? kPhSumOK<TY, NN, EE> : kPSumOK<TY, NN, EE>;
     NW_FUSED_TABLE(NW_PS)
 #undef NW_PS
     return false;
@@ -760,9 +771,11 @@ hipError_t fused_power_partials(const WDesc& d, int dtype, bool phase, const voi
                                 void* partials, int64_t nsig, hipStream_t s) {
 #define NW_PSL(TY, NN, EE)                                                                                    \
     if (d.n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) {                                          \
-        if constexpr (kPSumOK<TY, NN, EE>) {                                                                  \
+        if constexpr (kPhSumOK<TY, NN, EE>) {                                                                 \
             if (phase) return launch_psum<TY, NN, EE, kOutPhSum>(d, X, wtab, partials, nsig, s);              \
-            return launch_psum<TY, NN, EE, kOutPSum>(d, X, wtab, partials, nsig, s);                          \
+        }                                                                                                     \
+        if constexpr (kPSumOK<TY, NN, EE>) {                                                                  \
+            if (!phase) return launch_psum<TY, NN, EE, kOutPSum>(d, X, wtab, partials, nsig, s);              \
         }                                                                                                     \
         return hipErrorNotSupported;                                                                          \
     }

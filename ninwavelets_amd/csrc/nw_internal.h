@@ -178,11 +178,12 @@ int        fused_kernel_id(int64_t n, int dtype, int kind);   // NW_K_FUSED or N
 // forward R2C of nsig real rows of length n (fused sizes) into half spectra of row stride nh
 hipError_t fused_forward(int64_t n, int dtype, const void* x, void* X, int64_t nsig, int64_t nh, hipStream_t s);
 hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 pi i j / n), cached per device
-// epoch reduction partials (fused sizes, fp32 analytic rows, E <= 16): per block of signals
-// the sum over its signals (fp64, in signal order) of |y|^2, or with phase of y / |y|; one
+// epoch reduction partials (fused sizes, fp32 analytic rows; power up to E = 32, phase
+// E <= 16): per block of signals the sum over its signals (fp64, in signal order) of |y|^2,
+// or with phase of y / |y|; one
 // (groups, F, n) row of fp64 (phase: complex fp64) per (group, scale);
 // groups = fused_psum_groups(nsig)
-bool fused_psum_supported(int64_t n, int dtype, int kind);
+bool fused_psum_supported(int64_t n, int dtype, int kind, bool phase);
 int64_t fused_psum_groups(int64_t nsig);
 hipError_t fused_power_partials(const WDesc& d, int dtype, bool phase, const void* X, const void* wtab,
                                 void* partials, int64_t nsig, hipStream_t s);

@@ -153,11 +153,10 @@ def test_interpolate_at_n16384(dtype):
     assert max_err(got, ref) <= (1e-12 if dtype == 'float64' else 1e-5)
 
 
-@pytest.mark.parametrize('n', [1024, 2048, 4096])
+@pytest.mark.parametrize('n', [1024, 2048, 4096, 8192, 16384])
 def test_power_mean_fused_partials(n):
-    """fp32 epoch power sums at the register-resident fused sizes: the kernel sums |y|^2 over
-    each block of 8 signals in fp64 (nw_fused_kernel, kOutPSum) and the accumulator adds the
-    fp64 partials.  Against the mean of the same plan's per-signal power, which runs on the
+    """fp32 epoch power sums at the fused sizes: the kernel sums |y|^2 over each block of 8
+    signals in fp64 (nw_fused_kernel, kOutPSum) and the accumulator adds the fp64 partials.  Against the mean of the same plan's per-signal power, which runs on the
     pair kernel (its own fp32 rounding of y: 1e-6 of each point), ragged chunks (37 signals in
     chunks of 16 -> 16, 16, 5); chunk-size independent (the same fp64 additions of the same
     fp32 values, regrouped: 1e-13)."""

@@ -1,13 +1,13 @@
 """A/B of the fused epoch power partials: power_mean vs per-signal power on device tensors,
 the library given by NINWAVE_LIB (base: fused partials, _nopsum: power + accumulate)."""
-import sys, time
+import os, sys, time
 import numpy as np
 import torch
 import ninwavelets_amd as nw
 from ninwavelets_amd import _lib as L
 
 tag = sys.argv[1]
-for n in (1024, 2048, 4096):
+for n in [int(v) for v in os.environ.get('NS', '1024 2048 4096').split()]:
     S, F = 512, 256
     g = L.trans_grid(n / 1000., 1000., False)
     plan = nw.Plan(n, F, 'float32', max_batch=128)
