@@ -496,7 +496,7 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
             p->wtab_valid = true;
         }
         if (out_kind == OUT_PSUM || out_kind == OUT_PHSUM) {
-            p->stats.kernel = NW_K_FUSED;
+            p->stats.kernel = nw::fused_psum_kernel_id(p->n, p->dtype, out_kind == OUT_PHSUM);
             return staged(p, ST_FUSED, [&] {
                 NW_HIP(nw::fused_power_partials(p->desc, p->dtype, out_kind == OUT_PHSUM, p->d_X, p->d_wtab, dst, c,
                                                 p->stream));

@@ -855,9 +855,25 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
             // acc[q*R + i] += |y|^2 of output bfly(t, q) + bitrev(i)*NS (the same positions for
             // every signal of the block): the power output's value, added in fp64 in signal order
             // like k_accumulate, so the partials reproduce its sums
-            static_assert(!PAIRSIG, "partial sums run the single-signal kernel");
+            if constexpr (PAIRSIG) {
+                // signal s (low halves), then s + 1 (high halves) when the pair has one: the
+                // pair kernel's power-output values, in signal order
 #pragma unroll
-            for (int e = 0; e < Q * R; ++e) acc[e] += (double)(v[e].re * v[e].re + v[e].im * v[e].im);
+                for (int e = 0; e < Q * R; ++e) {
+                    const C2<S> a{v[e].re.x, v[e].im.x};
+                    acc[e] += (double)(a.re * a.re + a.im * a.im);
+                }
+                if (ocur2) {
+#pragma unroll
+                    for (int e = 0; e < Q * R; ++e) {
+                        const C2<S> b{v[e].re.y, v[e].im.y};
+                        acc[e] += (double)(b.re * b.re + b.im * b.im);
+                    }
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < Q * R; ++e) acc[e] += (double)(v[e].re * v[e].re + v[e].im * v[e].im);
+            }
         } else if constexpr (I::LAST && OUT == kOutPhSum) {
             static_assert(!PAIRSIG, "partial sums run the single-signal kernel");
 #pragma unroll

@@ -313,8 +313,11 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
 #ifndef NW_WPS_PAIR
 #define NW_WPS_PAIR 4
 #endif
+#ifndef NW_WPS_PAIR_PSUM
+#define NW_WPS_PAIR_PSUM 3   // + E fp64 power accumulators
+#endif
 template <int N, int E, int OUT>
-__global__ __launch_bounds__(N / E, NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc d, const cplx<float>* __restrict__ X,
+__global__ __launch_bounds__(N / E, OUT == kOutPSum ? NW_WPS_PAIR_PSUM : NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc d, const cplx<float>* __restrict__ X,
                                                                   const void* __restrict__ wtab, void* __restrict__ out,
                                                                   const C2<float>* __restrict__ tw, int64_t nsig,
                                                                   int group, int nsg_pad, const int* __restrict__ wnz) {
@@ -353,6 +356,13 @@ __global__ __launch_bounds__(N / E, NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc
     const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? dma_rounds_for<float>(nzv) : 1 << 30;
     C2<float> nyqa{0.0f, 0.0f}, nyqb{0.0f, 0.0f};
     auto xrow = [&](int64_t s) { return reinterpret_cast<const C2<float>*>(X + s * d.nh); };
+    // power partial sums (kOutPSum): as nw_fused_kernel, both signals of a pair into one sum
+    constexpr bool PSUM = OUT == kOutPSum;
+    double acc[PSUM ? E : 1];
+    if constexpr (PSUM) {
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = 0.0;
+    }
     if constexpr (PXD) {
         const int64_t s2 = s_begin + 1 < s_end ? s_begin + 1 : s_begin;
         nyqa = xrow(s_begin)[N / 2];
@@ -423,7 +433,15 @@ __global__ __launch_bounds__(N / E, NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc
         void* o1 = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;
         void* o2 = two ? (void*)((char*)out + (s2 * d.nfreq + fi) * (int64_t)N * out_esz) : nullptr;
         passes_from<f2, N, E, OUT, 1, PXD>(v, lds, t, tw, nullptr, reinterpret_cast<const C2<f2>*>(xn1), o1,
-                                           nullptr, o2, dma_rounds, xn2);
+                                           nullptr, o2, dma_rounds, xn2, PSUM ? acc : nullptr);
+    }
+    if constexpr (PSUM) {
+        using IL = PassInfo<N, E, G::npass() - 1, (int)sizeof(float), true>;
+        double* prow = reinterpret_cast<double*>(out) + ((int64_t)sg * d.nfreq + fi) * (int64_t)N;
+#pragma unroll
+        for (int q = 0; q < IL::Q; ++q)
+#pragma unroll
+            for (int i = 0; i < IL::R; ++i) prow[IL::bfly(t, q) + bitrev<IL::R>(i) * IL::NS] = acc[q * IL::R + i];
     }
 }
 
@@ -610,6 +628,9 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     return hipGetLastError();
 }
 
+#ifndef NW_PAIR_PSUM
+#define NW_PAIR_PSUM 1
+#endif
 template <typename T, int N, int E, int OUT>
 hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* partials, int64_t nsig, hipStream_t s) {
     constexpr int threads = N / E;
@@ -628,6 +649,17 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
     if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
     const int* wnz = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
                                                   wtab_row_bytes(N, d.nfreq, sizeof(T), true));
+    if constexpr (OUT == kOutPSum && NW_PAIR_PSUM && kPairMode<T, E, true>) {
+        // power partials on the signal-pair kernel: the same values as its power output
+        const int lp = kLdsBytes<f2, N, E>;
+        e = hipFuncSetAttribute((const void*)nw_fused_pair_kernel<N, E, kOutPSum>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, lp);
+        if (e != hipSuccess) return e;
+        nw_fused_pair_kernel<N, E, kOutPSum><<<blocks, threads, lp, s>>>(
+            d, reinterpret_cast<const cplx<float>*>(X), wtab, partials, reinterpret_cast<const C2<float>*>(tw), nsig,
+            kGroup, (int)nsg_pad, wnz);
+        return hipGetLastError();
+    }
     nw_fused_kernel<T, N, E, OUT, true><<<blocks, threads, lds, s>>>(
         d, reinterpret_cast<const cplx<T>*>(X), wtab, partials, reinterpret_cast<const C2<T>*>(tw), nsig, kGroup,
         (int)nsg_pad, wnz);
@@ -766,6 +798,15 @@ bool fused_psum_supported(int64_t n, int dtype, int kind, bool phase) {
 }
 
 int64_t fused_psum_groups(int64_t nsig) { return (nsig + kGroup - 1) / kGroup; }
+
+int fused_psum_kernel_id(int64_t n, int dtype, bool phase) {
+#define NW_PK_ID(TY, NN, EE) \
+    if (n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) \
+        return (!phase && NW_PAIR_PSUM && kPairMode<TY, EE, true>) ? NW_K_FUSED_PAIR : NW_K_FUSED;
+    NW_FUSED_TABLE(NW_PK_ID)
+#undef NW_PK_ID
+    return NW_K_NONE;
+}
 
 hipError_t fused_power_partials(const WDesc& d, int dtype, bool phase, const void* X, const void* wtab,
                                 void* partials, int64_t nsig, hipStream_t s) {

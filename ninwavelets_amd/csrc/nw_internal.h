@@ -185,6 +185,7 @@ hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 p
 // groups = fused_psum_groups(nsig)
 bool fused_psum_supported(int64_t n, int dtype, int kind, bool phase);
 int64_t fused_psum_groups(int64_t nsig);
+int fused_psum_kernel_id(int64_t n, int dtype, bool phase);   // NW_K_FUSED or NW_K_FUSED_PAIR
 hipError_t fused_power_partials(const WDesc& d, int dtype, bool phase, const void* X, const void* wtab,
                                 void* partials, int64_t nsig, hipStream_t s);
 
