@@ -192,10 +192,16 @@ def free_port() -> int:
     return port
 
 
-def launch_ranks(nranks: int, argv) -> int:
+PG_TIMEOUT_S = 120      # process-group rendezvous / collective timeout (a lost rank fails the run)
+
+
+def launch_ranks(nranks: int, argv, poll_s: float = 0.2) -> int:
     """Parent of an N-rank run started without torchrun: it never touches the GPU (no
-    torch import), starts one fresh child per rank, forwards rank 0's stdout and returns
-    the first non-zero exit status (children are never exec'd from a GPU process)."""
+    torch import), starts one fresh child per rank (children are never exec'd from a GPU
+    process) and forwards rank 0's stdout.  Every child is polled: the first one that exits
+    non-zero has its siblings terminated (a rank waiting in a rendezvous for a dead peer
+    would otherwise hang until the driver's time limit) and its exit status is returned."""
+    import threading
     port = free_port()
     procs = []
     for r in range(nranks):
@@ -203,15 +209,227 @@ def launch_ranks(nranks: int, argv) -> int:
                    LOCAL_WORLD_SIZE=str(nranks), MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, '-u', os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=subprocess.PIPE if r == 0 else subprocess.DEVNULL))
-    out0 = procs[0].stdout.read().decode()
-    rcs = [p.wait() for p in procs]
-    for ln in out0.splitlines():              # the JSON line to stdout, library chatter to stderr
+    out0 = []
+    reader = threading.Thread(target=lambda: out0.append(procs[0].stdout.read().decode()), daemon=True)
+    reader.start()
+    failed = None
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [(r, rc) for r, rc in enumerate(rcs) if rc not in (None, 0)]
+        if bad:
+            failed = bad[0]
+            break
+        if all(rc == 0 for rc in rcs):
+            break
+        time.sleep(poll_s)
+    if failed is not None:
+        log(f'[bench] rank {failed[0]} exited with {failed[1]}: terminating the other ranks')
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=10)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    reader.join(timeout=10)
+    for ln in ''.join(out0).splitlines():      # the JSON line to stdout, library chatter to stderr
         (sys.stdout if ln.startswith('{') else sys.stderr).write(ln + '\n')
     sys.stdout.flush()
-    bad = [rc for rc in rcs if rc != 0]
-    if bad:
+    rcs = [p.returncode for p in procs]
+    if failed is not None:
         log(f'[bench] rank exit codes: {rcs}')
-    return bad[0] if bad else 0
+        return failed[1] if failed[1] > 0 else 1
+    return 0
+
+
+# VALU peaks (MI355X_MICROARCH.md chip table: FP32 vector 157.3 TFLOPS spec; FP64 vector is
+# half the FP32 rate on gfx950, 78.6 TFLOPS spec)
+PEAK_VALU_TFLOPS = {'float32': 157.3, 'float64': 78.6}
+
+
+def fft_flops_per_row(n: int, kname: str) -> float:
+    """Nominal flops of one (signal, scale) row on the dominant kernel: 5 n log2 n for the
+    inverse FFT (the radix-2 operation count), + 2 n for the real-W x complex-X product.
+    The chirp-z form runs two M-point transforms per row (M = 2^ceil(log2(2n - 1)))."""
+    import math
+    if kname == 'nw_chirp_kernel':
+        m = 1 << (2 * n - 1).bit_length()
+        return 2 * 5.0 * m * math.log2(m) + 2.0 * n
+    return 5.0 * n * math.log2(n) + 2.0 * n
+
+
+def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg, dtype_override=None, fp64_leg=False):
+    """One measured workload: warmup, barrier-bracketed timed steps, max over ranks.
+    Returns (line fields, plan stats, extra) for rank 0's JSON line."""
+    kind, epochs, chans, n, freqs, out_kind, dtype, text = cfg
+    if args.epochs:
+        epochs = args.epochs
+    if args.output:
+        out_kind = args.output
+    if args.samples:
+        n = args.samples
+    if args.wavelet and args.wavelet != kind:
+        text = text.replace(kind.capitalize(), args.wavelet.capitalize(), 1)
+        kind = args.wavelet
+        if kind == 'shannon':
+            text += (' [Shannon ignores the freq (wavelets.py:256-262): its one distinct row is '
+                     'computed once per signal and copied to every scale]')
+    want = dtype_override or args.dtype
+    if want and want != dtype:
+        dtype = want
+        text = (text.replace('complex64 out', 'complex128 out') if fp64_leg else
+                text + f' [compute dtype overridden: {dtype}, outputs in {dtype} / its complex type]')
+    S = epochs * chans                       # signals on this rank
+    F = len(freqs)
+    F_all, by_scales = F, args.shard == 'scales' and world > 1
+    if by_scales:                            # this rank: a contiguous slice of the scales
+        from ninwavelets_amd.dist import shard
+        f0, f1 = shard(F, rank, world)
+        freqs = freqs[f0:f1]
+        F = f1 - f0
+    C = min(args.chunk or DEFAULT_CHUNK.get(args.config, 256), S)
+    f64 = dtype == 'float64'
+    x = synth_device(torch, S, n, seed=1000 + (0 if by_scales else rank), device=dev,
+                     dtype=torch.float64 if f64 else torch.float32)
+    odt = {('cwt', False): torch.complex64, ('cwt', True): torch.complex128}.get(
+        (out_kind, f64), torch.float64 if f64 else torch.float32)
+    bufs = [torch.empty((C, F, n), dtype=odt, device=dev) for _ in range(1 if C >= S else 2)]
+    plan = nw.Plan(n, F, dtype, device=dev.index, max_batch=C,
+                   engine=None if args.engine == 'auto' else args.engine, timing=True)
+    grid = L.trans_grid(n / 1000., 1000., False)
+    params = {'morse': [17.5, 3.0], 'morlet': [7.0, 0.0], 'shannon': []}[kind]
+    plan.set_wavelet(kind, params, freqs, grid)
+    esz = 8 if f64 else 4
+    x_ptr, x_row = x.data_ptr(), n * esz
+
+    def step():
+        for i, s0 in enumerate(range(0, S, C)):
+            c = min(C, S - s0)
+            plan.execute_ptr(x_ptr + s0 * x_row, c, bufs[i % len(bufs)].data_ptr(), out_kind)
+
+    def barrier():
+        torch.cuda.synchronize()
+        plan.sync()
+        if world > 1:
+            dist.barrier()
+
+    log(f'[bench] rank {rank}/{world} {args.config}{" fp64 leg" if fp64_leg else ""}: S={S} n={n} F={F} '
+        f'chunk={C} dtype={dtype} engine={plan.stats()["engine"]} device={dev}')
+    for w in range(args.warmup):
+        step()
+        barrier()
+        log(f'[bench] warmup {w + 1}/{args.warmup} done')
+    plan.reset_stats()
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step()
+    barrier()
+    el = time.perf_counter() - t0
+    el = max_over_ranks(torch, dist, el, world, dev if backend == 'nccl' else None)
+    st = plan.stats()
+    points = float(S) * F_all * n * args.steps * (1 if by_scales else world)
+    res = {'value': points / el, 'ms_per_step': el / args.steps * 1e3, 'dtype': 'f64' if f64 else 'f32',
+           'workload': text, 'kind': kind, 'epochs': epochs * (1 if by_scales else world), 'chans': chans,
+           'n': n, 'freqs': freqs, 'F': F, 'F_all': F_all, 'out_kind': out_kind, 'chunk': C,
+           'by_scales': by_scales, 'dtype_name': dtype}
+    extra = roofline_of(args, st, S, F, n, C, out_kind, dtype, esz, el, L) if rank == 0 else {}
+    plan.close()
+    del bufs, x
+    torch.cuda.empty_cache()
+    return res, st, extra
+
+
+def roofline_of(args, st, S, F, n, C, out_kind, dtype, esz, el, L):
+    """The dominant kernel's HBM roofline (event-timed average launch, algorithmic bytes),
+    its VALU roofline (nominal FFT flops) and the end-to-end figures."""
+    f64 = dtype == 'float64'
+    # dominant kernel: the fused kernel, or K1 (the spectrum multiply) on the rocFFT engine
+    fused = st['engine'] == 'fused'
+    two_pass = fused and st['launches_rows'] > 0     # n > 16384: nw_large.hip
+    launches = st['launches_fused'] if fused else st['launches_multiply']
+    ms = (st['ms_fused'] if fused else st['ms_multiply']) / max(1, launches)
+    out_e = (2 if out_kind == 'cwt' else 1) * esz
+    if not fused:
+        out_e = 2 * esz                    # K1 always writes the complex product
+    extra = {}
+    uniq = st['unique_rows']
+    rows_launch = float(S) * F * args.steps / max(1, launches)     # (signal, scale) rows per launch
+    if uniq < F and st['launches_expand'] > 0:
+        # repeated rows (Shannon): the engine computed `uniq` rows per signal and
+        # k_expand_rows wrote every output row, reading each computed row once -- the
+        # expand kernel moves the dominant bytes
+        comp_ms = (st['ms_fused'] + st['ms_rows'] + st['ms_multiply'] + st['ms_inverse'] +
+                   st['ms_epilogue']) / args.steps
+        extra['computed_rows'] = {'unique_rows': uniq, 'engine_ms_per_step': round(comp_ms, 3),
+                                  'engine_launches': launches}
+        ex_l = st['launches_expand']
+        ms = st['ms_expand'] / ex_l
+        out_e = (2 if out_kind == 'cwt' else 1) * esz
+        per_launch = float(S) * F * n * args.steps / ex_l * out_e * (1 + uniq / F)
+        kname = 'k_expand_rows'
+        rows_launch = 0.0
+    elif two_pass:
+        # column pass (the kernel that writes the output): reads B once (2e B/pt, complex
+        # in the compute dtype) and writes each output point once; the row pass writes B
+        # once and reads the transposed spectrum Xt once per launch (from L2 across the
+        # scales of a tile)
+        b_e = 2 * esz
+        pts_launch = float(S) * F * n * args.steps / max(1, launches)
+        per_launch = pts_launch * (b_e + out_e)
+        rows_l = max(1, st['launches_rows'])
+        rows_pts = float(S) * F * n * args.steps / rows_l
+        rows_bytes = rows_pts * b_e + n * b_e
+        rows_ms = st['ms_rows'] / rows_l
+        kname = 'cols_kernel'
+        extra['roofline_rows'] = {
+            'kernel': 'rows_kernel', 'bound': 'hbm',
+            'achieved': round(rows_bytes / (rows_ms * 1e-3) / 1e9, 1), 'peak': PEAK_HBM_GBPS,
+            'unit': 'GB/s', 'frac': round(rows_bytes / (rows_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
+            'avg_launch_ms': round(rows_ms, 4), 'algorithmic_bytes_per_launch': rows_bytes}
+    else:
+        per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
+        kname = L.KERNEL_NAMES[st['kernel']]          # the kernel rocprofv3 shows for this launch
+    if two_pass or kname == 'k_expand_rows':
+        # end to end against the path's minimum traffic (X read once, every output once)
+        oe = (2 if out_kind == 'cwt' else 1) * esz
+        min_bytes = float(S) * ((n // 2 + 1) * 2 * esz + F * n * oe)
+        extra['end_to_end_min_traffic'] = {
+            'bytes_per_step': min_bytes,
+            'achieved': round(min_bytes / (el / args.steps) / 1e9, 1), 'unit': 'GB/s',
+            'frac': round(min_bytes / (el / args.steps) / 1e9 / PEAK_HBM_GBPS, 4)}
+    achieved = per_launch / (ms * 1e-3) / 1e9
+    traffic, traffic_src = pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind, n)
+    roof = {'kernel': kname, 'bound': 'hbm',
+            'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
+            'frac': round(achieved / PEAK_HBM_GBPS, 4),
+            'traffic': traffic,
+            'traffic_source': (f'{traffic_src}: rocprofv3 PMC passes of this command, 2*FETCH_SIZE + '
+                               f'WRITE_SIZE per launch, on engine sources {source_hash()}'
+                               if traffic_src else 'no PMC summary on the current engine sources'),
+            'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
+    if rows_launch > 0 and kname in ('nw_fused_kernel', 'nw_fused_pair_kernel', 'nw_chirp_kernel', 'cols_kernel'):
+        # the other roof: nominal FFT flops of the rows this kernel finishes per launch (the
+        # two-pass form's flops are split between its row and column passes: both counted
+        # against the column pass's time would overstate it, so it is priced per step)
+        fl = fft_flops_per_row(n, kname)
+        if two_pass:
+            t_s, flops, what = el / args.steps, float(S) * F * fl, 'per step (row + column passes)'
+        else:
+            t_s, flops, what = ms * 1e-3, rows_launch * fl, 'per launch'
+        tf = flops / t_s / 1e12
+        extra['valu_roofline'] = {
+            'kernel': kname, 'bound': 'valu', 'achieved': round(tf, 2), 'peak': PEAK_VALU_TFLOPS[dtype],
+            'unit': 'TFLOP/s', 'frac': round(tf / PEAK_VALU_TFLOPS[dtype], 4),
+            'flops': flops, 'flops_basis': f'5 n log2 n + 2 n per (signal, scale) row {what} '
+                                           f'(nominal radix-2 count; pruned rows do less)'}
+    extra['stage_ms_per_step'] = {k: round(st[k] / args.steps, 3) for k in
+                                  ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_rows',
+                                   'ms_expand', 'ms_copy')}
+    extra['roofline'] = roof
+    return extra
 
 
 def main(argv=None):
@@ -238,12 +456,19 @@ def main(argv=None):
                          'or the scale list of the same signals (strong scaling; the C5 split for '
                          'one long signal, SURVEY §8e)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-fp64', action='store_true',
+                    help='skip the fp64 leg (the same workload at the reference\'s complex128 precision, '
+                         'reported under the "fp64" key of the default C4 line)')
     ap.add_argument('--backend', default=None, choices=['nccl', 'gloo'],
                     help='process-group backend for N > 1 ranks (default: nccl = RCCL over xGMI; '
                          'gloo with --dry-run)')
+    ap.add_argument('--same-device', action='store_true',
+                    help='rank r uses device LOCAL_RANK %% device_count (several ranks share a GPU: the '
+                         'multi-rank path with real kernels on a 1-GPU box; use --backend gloo)')
     ap.add_argument('--dry-run', action='store_true',
                     help='no GPU and no kernels: exercise the launcher, the process group, the '
                          'barriers and the max-over-ranks timing on CPU (tests)')
+    ap.add_argument('--fail-rank', type=int, default=None, help=argparse.SUPPRESS)   # tests: that rank exits 3
     args = ap.parse_args(argv)
 
     if 'WORLD_SIZE' in os.environ:           # torchrun or our own launcher: this process is a rank
@@ -257,177 +482,72 @@ def main(argv=None):
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     backend = args.backend or ('gloo' if args.dry_run else 'nccl')
+    if args.fail_rank is not None and args.fail_rank == rank:
+        log(f'[bench] rank {rank}: --fail-rank, exiting with 3 before the rendezvous')
+        return 3
 
+    import datetime
     import torch
     import torch.distributed as dist
+    timeout = datetime.timedelta(seconds=PG_TIMEOUT_S)
     if args.dry_run:
-        return dry_run(args, torch, dist, world, rank, backend)
+        return dry_run(args, torch, dist, world, rank, backend, timeout)
     import ninwavelets_amd as nw
     from ninwavelets_amd import _lib as L
 
+    if args.same_device:
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         torch.cuda.set_device(local)
         if backend == 'nccl':
-            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=timeout)
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
-    kind, epochs, chans, n, freqs, out_kind, dtype, text = CONFIGS[args.config]
-    if args.epochs:
-        epochs = args.epochs
-    if args.output:
-        out_kind = args.output
-    if args.samples:
-        n = args.samples
-    if args.wavelet and args.wavelet != kind:
-        text = text.replace(kind.capitalize(), args.wavelet.capitalize(), 1)
-        kind = args.wavelet
-        if kind == 'shannon':
-            text += (' [Shannon ignores the freq (wavelets.py:256-262): its one distinct row is '
-                     'computed once per signal and copied to every scale]')
-    if args.dtype and args.dtype != dtype:
-        dtype = args.dtype
-        text += f' [compute dtype overridden: {dtype}, outputs in {dtype} / its complex type]'
-    S = epochs * chans                       # signals on this rank
-    F = len(freqs)
-    F_all, by_scales = F, args.shard == 'scales' and world > 1
-    if by_scales:                            # this rank: a contiguous slice of the scales
-        from ninwavelets_amd.dist import shard
-        f0, f1 = shard(F, rank, world)
-        freqs = freqs[f0:f1]
-        F = f1 - f0
-    C = min(args.chunk or DEFAULT_CHUNK.get(args.config, 256), S)
-    f64 = dtype == 'float64'
-    x = synth_device(torch, S, n, seed=1000 + (0 if by_scales else rank), device=dev, dtype=torch.float64 if f64 else torch.float32)
-    odt = {('cwt', False): torch.complex64, ('cwt', True): torch.complex128}.get(
-        (out_kind, f64), torch.float64 if f64 else torch.float32)
-    bufs = [torch.empty((C, F, n), dtype=odt, device=dev) for _ in range(1 if C >= S else 2)]
-    plan = nw.Plan(n, F, dtype, device=local, max_batch=C,
-                   engine=None if args.engine == 'auto' else args.engine, timing=True)
-    grid = L.trans_grid(n / 1000., 1000., False)
-    params = {'morse': [17.5, 3.0], 'morlet': [7.0, 0.0], 'shannon': []}[kind]
-    plan.set_wavelet(kind, params, freqs, grid)
-    esz = 8 if f64 else 4
-    x_ptr, x_row = x.data_ptr(), n * esz
-
-    def step():
-        for i, s0 in enumerate(range(0, S, C)):
-            c = min(C, S - s0)
-            plan.execute_ptr(x_ptr + s0 * x_row, c, bufs[i % len(bufs)].data_ptr(), out_kind)
-
-    def barrier():
-        torch.cuda.synchronize()
-        plan.sync()
-        if world > 1:
-            dist.barrier()
-
-    log(f'[bench] rank {rank}/{world} {args.config}: S={S} n={n} F={F} chunk={C} '
-        f'engine={plan.stats()["engine"]}')
-    for w in range(args.warmup):
-        step()
-        barrier()
-        log(f'[bench] warmup {w + 1}/{args.warmup} done')
-    plan.reset_stats()
-    barrier()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        step()
-    barrier()
-    el = time.perf_counter() - t0
-    el = max_over_ranks(torch, dist, el, world, dev if backend == 'nccl' else None)
-    st = plan.stats()
-    points = float(S) * F_all * n * args.steps * (1 if by_scales else world)
-    value = points / el
+    res, st, extra = run_leg(args, torch, dist, nw, L, world, rank, dev, backend, CONFIGS[args.config])
+    # the reference's own precision (complex128, base.py:399-406): the default C4 line also
+    # carries the same workload computed in fp64, with its own roofline
+    fp64 = None
+    want_fp64 = (args.config == 'c4' and res['dtype'] == 'f32' and not args.no_fp64 and not args.dtype and
+                 not args.output and not args.samples and not args.wavelet)
+    if want_fp64:
+        r64, st64, ex64 = run_leg(args, torch, dist, nw, L, world, rank, dev, backend, CONFIGS[args.config],
+                                  dtype_override='float64', fp64_leg=True)
+        if rank == 0:
+            fp64 = {'value': r64['value'], 'unit': 'points/s', 'ms_per_step': r64['ms_per_step'], 'dtype': 'f64',
+                    'workload': r64['workload'], 'chunk_signals': r64['chunk'], 'engine': st64['engine'],
+                    'roofline': ex64['roofline'], 'valu_roofline': ex64.get('valu_roofline'),
+                    'stage_ms_per_step': ex64['stage_ms_per_step']}
 
     if rank == 0:
-        # dominant kernel: the fused kernel, or K1 (the spectrum multiply) on the rocFFT engine
-        fused = st['engine'] == 'fused'
-        two_pass = fused and st['launches_rows'] > 0     # n > 16384: nw_large.hip
-        launches = st['launches_fused'] if fused else st['launches_multiply']
-        ms = (st['ms_fused'] if fused else st['ms_multiply']) / max(1, launches)
-        out_e = (2 if out_kind == 'cwt' else 1) * esz
-        if not fused:
-            out_e = 2 * esz                    # K1 always writes the complex product
-        extra = {}
-        uniq = st['unique_rows']
-        if uniq < F and st['launches_expand'] > 0:
-            # repeated rows (Shannon): the engine computed `uniq` rows per signal and
-            # k_expand_rows wrote every output row, reading each computed row once -- the
-            # expand kernel moves the dominant bytes
-            comp_ms = (st['ms_fused'] + st['ms_rows'] + st['ms_multiply'] + st['ms_inverse'] +
-                       st['ms_epilogue']) / args.steps
-            extra['computed_rows'] = {'unique_rows': uniq, 'engine_ms_per_step': round(comp_ms, 3),
-                                      'engine_launches': launches}
-            ex_l = st['launches_expand']
-            ms = st['ms_expand'] / ex_l
-            out_e = (2 if out_kind == 'cwt' else 1) * esz
-            per_launch = float(S) * F * n * args.steps / ex_l * out_e * (1 + uniq / F)
-            kname = 'k_expand_rows'
-        elif two_pass:
-            # column pass (the kernel that writes the output): reads B once (2e B/pt, complex
-            # in the compute dtype) and writes each output point once; the row pass writes B
-            # once and reads the transposed spectrum Xt once per launch (from L2 across the
-            # scales of a tile)
-            b_e = 2 * esz
-            pts_launch = float(S) * F * n * args.steps / max(1, launches)
-            per_launch = pts_launch * (b_e + out_e)
-            rows_l = max(1, st['launches_rows'])
-            rows_pts = float(S) * F * n * args.steps / rows_l
-            rows_bytes = rows_pts * b_e + n * b_e
-            rows_ms = st['ms_rows'] / rows_l
-            kname = 'cols_kernel'
-            extra['roofline_rows'] = {
-                'kernel': 'rows_kernel', 'bound': 'hbm',
-                'achieved': round(rows_bytes / (rows_ms * 1e-3) / 1e9, 1), 'peak': PEAK_HBM_GBPS,
-                'unit': 'GB/s', 'frac': round(rows_bytes / (rows_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
-                'avg_launch_ms': round(rows_ms, 4), 'algorithmic_bytes_per_launch': rows_bytes}
-        else:
-            per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
-            kname = L.KERNEL_NAMES[st['kernel']]          # the kernel rocprofv3 shows for this launch
-        if two_pass or kname == 'k_expand_rows':
-            # end to end against the path's minimum traffic (X read once, every output once)
-            oe = (2 if out_kind == 'cwt' else 1) * esz
-            min_bytes = float(S) * ((n // 2 + 1) * 2 * esz + F * n * oe)
-            extra['end_to_end_min_traffic'] = {
-                'bytes_per_step': min_bytes,
-                'achieved': round(min_bytes / (el / args.steps) / 1e9, 1), 'unit': 'GB/s',
-                'frac': round(min_bytes / (el / args.steps) / 1e9 / PEAK_HBM_GBPS, 4)}
-        achieved = per_launch / (ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind, n)
-        roof = {'kernel': kname, 'bound': 'hbm',
-                'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
-                'frac': round(achieved / PEAK_HBM_GBPS, 4),
-                'traffic': traffic,
-                'traffic_source': (f'{traffic_src}: rocprofv3 PMC passes of this command, 2*FETCH_SIZE + '
-                                   f'WRITE_SIZE per launch, on engine sources {source_hash()}'
-                                   if traffic_src else 'no PMC summary on the current engine sources'),
-                'avg_launch_ms': round(ms, 4), 'algorithmic_bytes_per_launch': per_launch}
-        stage_ms = {k: round(st[k] / args.steps, 3) for k in
-                    ('ms_forward', 'ms_multiply', 'ms_inverse', 'ms_epilogue', 'ms_fused', 'ms_rows', 'ms_expand',
-                     'ms_copy')}
         cpu = cpu_pool = None
         if world == 1 and not args.no_cpu_baseline:
             log('[bench] cpu baseline ...')
-            cpu = cpu_baseline(kind, n, freqs, out_kind)
+            cpu = cpu_baseline(res['kind'], res['n'], res['freqs'], res['out_kind'])
             for k in ('sample_seconds', 'rows_done'):
                 cpu.pop(k)
-            if n <= (1 << 16):
+            if res['n'] <= (1 << 16):
                 log('[bench] cpu baseline (process pool) ...')
-                cpu_pool = cpu_baseline_pool(kind, n, freqs, out_kind)
+                cpu_pool = cpu_baseline_pool(res['kind'], res['n'], res['freqs'], res['out_kind'])
+        roof = extra.pop('roofline')
+        stage_ms = extra.pop('stage_ms_per_step')
         line = {
             'metric': 'CWT throughput (epochs*chans*samples*freqs)/s',
-            'value': value, 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
-            'warmup': args.warmup, 'ms_per_step': el / args.steps * 1e3, 'higher_is_better': True,
-            'scaling': 'strong' if by_scales else 'weak', 'vs_baseline': None, 'dtype': 'f64' if f64 else 'f32', 'data': 'synthetic',
-            'config': {'workload': text, 'wavelet': kind, 'epochs': epochs * (1 if by_scales else world),
-                       'chans': chans, 'samples': n, 'freqs': F_all, 'output': out_kind, 'engine': st['engine'],
-                       'chunk_signals': C,
+            'value': res['value'], 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
+            'warmup': args.warmup, 'ms_per_step': res['ms_per_step'], 'higher_is_better': True,
+            'scaling': 'strong' if res['by_scales'] else 'weak', 'vs_baseline': None, 'dtype': res['dtype'],
+            'data': 'synthetic',
+            'config': {'workload': res['workload'], 'wavelet': res['kind'], 'epochs': res['epochs'],
+                       'chans': res['chans'], 'samples': res['n'], 'freqs': res['F_all'], 'output': res['out_kind'],
+                       'engine': st['engine'], 'chunk_signals': res['chunk'],
                        'parallelism': (f'scales{world} (each rank a contiguous slice of the scales, '
-                                       f'no collective)' if by_scales else
-                                       f'dp{world} (signals sharded, no collective)')},
-            'roofline': roof, **extra, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool, 'stage_ms_per_step': stage_ms,
+                                       f'no collective)' if res['by_scales'] else
+                                       f'dp{world} (signals sharded, no collective)'),
+                       **({'backend': backend, 'same_device': True} if args.same_device else {})},
+            'roofline': roof, **extra, 'fp64': fp64, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool,
+            'stage_ms_per_step': stage_ms,
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -444,12 +564,12 @@ def max_over_ranks(torch, dist, el, world, device):
     return float(t.item())
 
 
-def dry_run(args, torch, dist, world, rank, backend):
+def dry_run(args, torch, dist, world, rank, backend, timeout=None):
     """The multi-rank flow without a GPU: process group, warmup, barrier-bracketed timed
     steps (a fixed CPU stand-in per step), MAX over ranks, rank 0's line.  Its value is
     not a measurement; it proves the launcher and the rank plumbing (tests)."""
     if world > 1:
-        dist.init_process_group(backend)
+        dist.init_process_group(backend, **({'timeout': timeout} if timeout else {}))
     kind, epochs, chans, n, freqs, out_kind, dtype, text = CONFIGS[args.config]
 
     def step():

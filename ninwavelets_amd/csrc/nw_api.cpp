@@ -117,6 +117,13 @@ struct nw_plan {
     size_t d_out_bytes = 0;
     void* d_acc = nullptr;           // epoch reductions: fp64 (F, n) sums (x2 for phases)
     size_t d_acc_bytes = 0;
+    // nw_execute_multi_device reductions: this device's fp64 partial sums, and (device 0's
+    // plan) the peer-copy landing buffer; kept across calls (a hipFree per call would
+    // synchronise the device on every epoch-loop iteration)
+    void* d_part = nullptr;
+    size_t d_part_bytes = 0;
+    void* d_gather = nullptr;
+    size_t d_gather_bytes = 0;
     void* d_wtab = nullptr;          // fused engine: W[f, k] (pad_to + 1/n applied); n > 16384: kmax[f]
     size_t d_wtab_bytes = 0;
     bool wtab_valid = false;
@@ -691,7 +698,7 @@ void free_plan(nw_plan* p) {
     if (p->info) rocfft_execution_info_destroy(p->info);
     void* bufs[] = {p->work,   p->d_x,    p->d_X,        p->d_Y,     p->d_out,      p->d_wtab,
                     p->d_freq, p->d_peak, p->d_xstep32, p->d_table, p->d_row_len, p->d_acc, p->d_scratch,
-                    p->d_ubuf, p->d_rep,  p->d_uout, p->d_obuf, p->d_oscr};
+                    p->d_ubuf, p->d_rep,  p->d_uout, p->d_obuf, p->d_oscr, p->d_part, p->d_gather};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (auto& pe : p->pending) {
@@ -1267,27 +1274,16 @@ int nw_execute_multi_device(nw_plan* const* plans, int nplans, const void* const
     const bool phase = is_phase(out_kind);
     const int64_t fn = (int64_t)p0->nfreq * p0->n;
     const size_t acc_bytes = (size_t)fn * (phase ? 2 : 1) * sizeof(double);
-    // reductions: per-device fp64 partial sums, then device 0's gather buffer
+    // reductions: per-device fp64 partial sums (each plan's d_part), then device 0's gather
+    // buffer (plans[0]->d_gather); both persist on the plans and are freed with them
     std::vector<void*> part(nplans, nullptr);
-    void* gather = nullptr;
-    auto release = [&] {
-        for (int i = 0; i < nplans; ++i)
-            if (part[i]) {
-                DeviceGuard g(plans[i]->device);
-                (void)hipFree(part[i]);
-            }
-        if (gather) {
-            DeviceGuard g(p0->device);
-            (void)hipFree(gather);
-        }
-    };
     if (reduce) {
         for (int i = 0; i < nplans; ++i) {
             DeviceGuard g(plans[i]->device);
-            if (hipMalloc(&part[i], acc_bytes) != hipSuccess) {
-                release();
-                return fail(NW_E_NOMEM, "nw_execute_multi_device: partial-sum buffer");
-            }
+            const int r = ensure(&plans[i]->d_part, &plans[i]->d_part_bytes, acc_bytes);
+            if (r != NW_OK) return fail(r, "device " + std::to_string(plans[i]->device) +
+                                                ": nw_execute_multi_device: partial-sum buffer: " + g_last_error);
+            part[i] = plans[i]->d_part;
         }
     }
     std::vector<int> rc(nplans, NW_OK);
@@ -1304,10 +1300,7 @@ int nw_execute_multi_device(nw_plan* const* plans, int nplans, const void* const
     }
     for (auto& t : th) t.join();
     for (int i = 0; i < nplans; ++i)
-        if (rc[i] != NW_OK) {
-            release();
-            return fail(rc[i], "device " + std::to_string(plans[i]->device) + ": " + err[i]);
-        }
+        if (rc[i] != NW_OK) return fail(rc[i], "device " + std::to_string(plans[i]->device) + ": " + err[i]);
     if (!reduce) return NW_OK;
     int r = NW_OK;
     {
@@ -1319,7 +1312,11 @@ int nw_execute_multi_device(nw_plan* const* plans, int nplans, const void* const
         };
         const int64_t comps = fn * (phase ? 2 : 1);
         double* acc = (double*)part[0];
-        if (nplans > 1) hip(hipMalloc(&gather, acc_bytes), "hipMalloc");
+        void* gather = nullptr;
+        if (nplans > 1) {
+            r = ensure(&p0->d_gather, &p0->d_gather_bytes, acc_bytes);
+            gather = p0->d_gather;
+        }
         for (int i = 1; i < nplans && r == NW_OK; ++i) {
             if (hip(hipMemcpyPeerAsync(gather, p0->device, part[i], plans[i]->device, acc_bytes, p0->stream), "peer copy"))
                 hip(nw::launch_add_f64(acc, (const double*)gather, comps, p0->stream), "add");
@@ -1332,7 +1329,6 @@ int nw_execute_multi_device(nw_plan* const* plans, int nplans, const void* const
         }
         hip(hipStreamSynchronize(p0->stream), "sync");
     }
-    release();
     return r;
 }
 

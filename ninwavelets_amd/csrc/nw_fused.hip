@@ -173,7 +173,11 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
     auto w_at = [&](int r) -> WT {
         if constexpr (WREG) return w[r];
         else if (r < WKEEP) return wk[r < WKEEP ? r : 0];
+#ifdef NW_ABL_NOWLOAD   // diagnostic only (wrong results): W beyond WKEEP without its global loads
+        else { WT z{}; if constexpr (REALW) z = (T)(r + 1); return z; }
+#else
         else return *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
+#endif
     };
 
 #ifdef NW_STAMPS
@@ -223,7 +227,8 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
         if constexpr (XD || XB) {
             // this wave's DMA landed (only the stores issued after it may be pending),
             // then every wave's: the whole X[0 .. N/2) is in LDS
-            if (s == s_begin) wait_vmcnt<0>(); else wait_vmcnt<LastStores<T, N, E, OUT>::COUNT>();
+            // (the partial-sum modes store nothing after the DMA: nothing may stay pending)
+            if (s == s_begin || PSUM) wait_vmcnt<0>(); else wait_vmcnt<LastStores<T, N, E, OUT>::COUNT>();
             lds_barrier();
             xl = XD ? reinterpret_cast<const C2<T>*>(lds) : XBuf<T, N, E>::at_lds(lds);
         }

@@ -118,7 +118,7 @@ class Plan:
         if _is_device_tensor(x):
             if out is None:
                 raise ValueError('device execute needs an output tensor')
-            nsig = x.numel() // self.n
+            nsig = self._check_device_input(x)
             self._check_device_buffers(x, out, nsig, out_kind)
             with self._ordered_with_torch(x.device):
                 L.check(L.lib().nw_execute(self._h, ctypes.c_void_p(x.data_ptr()), nsig,
@@ -166,23 +166,42 @@ class Plan:
         L.check(L.lib().nw_execute(self._h, ctypes.c_void_p(x_ptr), int(nsig), ctypes.c_void_p(out_ptr),
                                    OUT_KINDS[out_kind], L.NW_MEM_DEVICE))
 
-    def _check_device_buffers(self, x, out, nsig, out_kind):
+    def _check_device_input(self, x) -> int:
+        """The input half of _check_device_buffers: a contiguous (nsig, n) tensor of the
+        compute dtype on the plan's device, whole rows only.  Returns nsig."""
         import torch
         want_x = torch.float32 if self.dtype == np.float32 else torch.float64
+        if not _is_device_tensor(x):
+            raise ValueError(f'device input must be a torch tensor on device {self.device}')
+        if x.dtype != want_x:
+            raise ValueError(f'device input must be {want_x}, got {x.dtype}')
+        if not x.is_contiguous():
+            raise ValueError('device input must be contiguous')
+        if x.numel() % self.n:
+            raise ValueError(f'device input of {x.numel()} values is not a whole number of '
+                             f'{self.n}-sample signals')
+        if x.device.index != self.device:
+            raise ValueError(f'device input must live on device {self.device}, got {x.device}')
+        return x.numel() // self.n
+
+    def _check_device_buffers(self, x, out, nsig, out_kind):
+        import torch
+        if self._check_device_input(x) != nsig:
+            raise ValueError('device buffer sizes do not match (S, n) -> (S, nfreq, n) / (nfreq, n)')
         want_o = {('cwt', np.float32): torch.complex64, ('cwt', np.float64): torch.complex128}.get(
-            (out_kind, self.dtype.type), want_x)
+            (out_kind, self.dtype.type), x.dtype)
         if out_kind == 'power_sum':
             want_o = torch.float64
         elif out_kind == 'phase_sum':
             want_o = torch.complex128
-        if x.dtype != want_x or out.dtype != want_o:
-            raise ValueError(f'device buffers must be {want_x} in / {want_o} out')
-        if not (x.is_contiguous() and out.is_contiguous()):
+        if out.dtype != want_o:
+            raise ValueError(f'device buffers must be {x.dtype} in / {want_o} out')
+        if not out.is_contiguous():
             raise ValueError('device buffers must be contiguous')
         rows = 1 if out_kind in REDUCTIONS else nsig
-        if x.numel() != nsig * self.n or out.numel() != rows * self.nfreq * self.n:
+        if out.numel() != rows * self.nfreq * self.n:
             raise ValueError('device buffer sizes do not match (S, n) -> (S, nfreq, n) / (nfreq, n)')
-        if x.device.index != self.device or out.device.index != self.device:
+        if out.device.index != self.device:
             raise ValueError(f'device buffers must live on device {self.device}')
 
     # -- misc --------------------------------------------------------------------
@@ -250,11 +269,11 @@ def execute_multi_device(plans, xs, outs, out_kind: str = 'cwt'):
     red = out_kind in REDUCTIONS
     nsig = []
     for i, (p, x, o) in enumerate(zip(plans, xs, outs)):
-        ns = x.numel() // p.n
-        if red:
-            if i == 0:
-                p._check_device_buffers(x, o, ns, out_kind)
-        else:
+        # every input is validated (dtype, contiguity, whole rows, device): its raw pointer
+        # goes to nw_execute as device memory of plan i; for the reductions only outs[0] is
+        # written, so the other outputs may be None
+        ns = p._check_device_input(x)
+        if not red or i == 0:
             p._check_device_buffers(x, o, ns, out_kind)
         nsig.append(ns)
     import torch

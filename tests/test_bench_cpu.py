@@ -62,3 +62,27 @@ def test_pmc_traffic_needs_current_sources(tmp_path, monkeypatch):
 
 def test_cpu_model_is_reported():
     assert isinstance(bench.cpu_model(), str) and bench.cpu_model()
+
+
+def test_launcher_fails_fast_when_a_rank_dies():
+    """Rank 1 exits 3 before the rendezvous: the launcher must notice, terminate rank 0
+    (which would otherwise wait for its peer until the process-group timeout) and return 3."""
+    import time
+    t0 = time.monotonic()
+    r = run('--gpus', '2', '--dry-run', '--steps', '2', '--warmup', '1', '--fail-rank', '1')
+    el = time.monotonic() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert el < bench.PG_TIMEOUT_S / 2, el
+    assert 'rank 1 exited with 3' in r.stderr
+    assert not [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+
+
+def test_launcher_fails_fast_when_rank0_dies():
+    r = run('--gpus', '3', '--dry-run', '--steps', '2', '--warmup', '1', '--fail-rank', '0')
+    assert r.returncode == 3, r.stderr[-2000:]
+
+
+def test_fft_flops_model():
+    # 5 n log2 n + 2 n per row; the chirp-z form: two M-point transforms, M = 2^ceil(log2(2n - 1))
+    assert bench.fft_flops_per_row(4096, 'nw_fused_pair_kernel') == 5 * 4096 * 12 + 2 * 4096
+    assert bench.fft_flops_per_row(1201, 'nw_chirp_kernel') == 2 * 5 * 4096 * 12 + 2 * 1201

@@ -27,7 +27,8 @@ for it in range(3):
     fn(buf, 1)
 names = ['pass0 load+dft', 'exch 0->1', 'pass1 dft', 'exch 1->2', 'pass2 dft', 'exch 2->3', 'pass3 dft', 'stores']
 tot = sum(buf[k] for k in range(8))
-sw = buf[8] * (n // (32 if (n == 16384 and dtype == 'float32') else 16) // 64)   # signal-waves
+E = 32 if n >= 8192 else 16          # NW_FUSED_TABLE: E = 32 at n = 8192 / 16384 (fp32 and fp64)
+sw = buf[8] * (n // E // 64)   # signal-waves
 print(f'n={n} F={F} {dtype} {out_kind}: signal-waves={sw}, cycles/signal/wave={tot / max(1, sw):.0f}')
 for k in range(8):
     if buf[k]:
