@@ -17,8 +17,10 @@
 #endif
 #ifndef NW_PACK_MAX
 #define NW_PACK_MAX 2      // measured (n = 4096): pairs of 8-B outputs 0.413 -> 0.403 ms (cwt);
-                           // quads of 4-B outputs 0.337 -> 0.360 ms (power): slower, so off
+                           // quads of 4-B outputs 0.337 -> 0.360 ms (power), pairs of them (8-B
+                           // stores) C3 1.253 -> 1.277 ms (round 3): slower, so 8-B outputs only
 #endif
+
 #ifndef NW_PRUNE
 #define NW_PRUNE 1         // pass 0 skips the elements beyond the W row's support
 #endif
@@ -354,9 +356,11 @@ __device__ __forceinline__ unsigned long long nw_now() {
 }
 #define NW_STAMP(st, k)                                 \
     do {                                                \
-        const unsigned long long now_ = nw_now();       \
-        (st)->acc[k] += now_ - (st)->last;              \
-        (st)->last = now_;                              \
+        if (st) {   /* callers without stamps pass nullptr (fwd_r2c, rows, chirp) */ \
+            const unsigned long long now_ = nw_now();   \
+            (st)->acc[k] += now_ - (st)->last;          \
+            (st)->last = now_;                          \
+        }                                               \
     } while (0)
 constexpr int kStampsStore = kStamps - 1;
 #else
@@ -878,15 +882,25 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
             static_assert(!PAIRSIG, "partial sums run the single-signal kernel");
 #pragma unroll
             for (int e = 0; e < Q * R; ++e) {
-                // |y|^2 of fp32 parts is exact in fp64 up to one rounding (no overflow), so
-                // rsqrt replaces hypot + two divisions (k_accumulate) to within a few fp64 ulp;
-                // y = 0 gives 0 * inf = NaN like the reference's 0/0 (mneutils.py:68)
                 const double re = (double)v[e].re, im = (double)v[e].im;
-                const double inv = NW_PHSUM_RSQ ? rsqrt(re * re + im * im) : 1.0 / hypot(re, im);
-                // products rounded before the add (no fma into acc): a partial then adds the
-                // same values whichever block boundaries the chunking draws
-                acc[2 * e] += mul_nocontract(re, inv);
-                acc[2 * e + 1] += mul_nocontract(im, inv);
+                if constexpr (sizeof(S) == 8) {
+                    // fp64 y: hypot, as k_accumulate (|y|^2 of fp64 parts can underflow: rows of
+                    // tiny magnitude, e.g. |y| ~ 1e-260 at the edge of a 1 Hz row), then one
+                    // reciprocal for both parts (within 1 ulp of its two divisions); y = 0 gives
+                    // 0 * inf = NaN like the reference's 0/0
+                    const double inv = 1.0 / hypot(re, im);
+                    acc[2 * e] += mul_nocontract(re, inv);
+                    acc[2 * e + 1] += mul_nocontract(im, inv);
+                } else {
+                    // |y|^2 of fp32 parts is exact in fp64 up to one rounding (no overflow), so
+                    // rsqrt replaces hypot + two divisions (k_accumulate) to within a few fp64
+                    // ulp; y = 0 gives 0 * inf = NaN like the reference's 0/0 (mneutils.py:68)
+                    const double inv = NW_PHSUM_RSQ ? rsqrt(re * re + im * im) : 1.0 / hypot(re, im);
+                    // products rounded before the add (no fma into acc): a partial then adds the
+                    // same values whichever block boundaries the chunking draws
+                    acc[2 * e] += mul_nocontract(re, inv);
+                    acc[2 * e + 1] += mul_nocontract(im, inv);
+                }
             }
         } else if constexpr (I::LAST && OUT == kOutXHalf) {
             // forward R2C: X[k] = conj(sum_n x[n] w^(+kn)) for k <= n/2 (row stride n/2 + 1)

@@ -119,8 +119,12 @@ template <typename T> constexpr int kTileGT = sizeof(T) == 8 ? NW_TILEG64 : NW_T
 #define NW_WPS_PSUM32 2
 #endif
 #define NW_WPS_OF(T, E, OUT) \
-    ((OUT) == kOutPhSum ? NW_WPS_PHSUM : ((OUT) == kOutPSum && (E) >= 32) ? NW_WPS_PSUM32 : NW_WAVES_PER_SIMD(T, E))
-template <typename T, int N, int E, int OUT, bool REALW>
+    (sizeof(T) == 8 ? NW_WPS64 : (OUT) == kOutPhSum ? NW_WPS_PHSUM : ((OUT) == kOutPSum && (E) >= 32) ? NW_WPS_PSUM32 \
+                                                                                                  : NW_WAVES_PER_SIMD(T, E))
+// WSH: the W-row support table wnz was built for the output kernels' E << WSH elements per
+// thread (the partial-sum kernels may run at a smaller E): a row whose elements r >= nz are
+// zero at E << WSH has elements r >= max(1, nz >> WSH) zero here
+template <typename T, int N, int E, int OUT, bool REALW, int WSH = 0>
 __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
                                                             const void* __restrict__ wtab, void* __restrict__ out,
                                                             const C2<T>* __restrict__ tw, int64_t nsig, int group,
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
     C2<T> nyq{T(0), T(0)};
     if constexpr (XD || XB) {
         nyq = reinterpret_cast<const C2<T>*>(X + s_begin * d.nh)[N / 2];
-        const int nz0 = NW_PRUNE ? wnz[fi] : E;
+        const int nz0 = NW_PRUNE ? max(1, wnz[fi] >> WSH) : E;
         const int nzv0 = nz0 < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz0;
         dma_x<T, N, G::T>(reinterpret_cast<const C2<T>*>(X + s_begin * d.nh),
                           XD ? (void*)lds : (void*)XBuf<T, N, E>::at_lds(lds), t,
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
     // W row support (device-built with the table): elements r >= nz of pass 0 multiply an
     // exactly-zero W for every thread of the block (k = t + r*T beyond the row's last
     // nonzero bin), so they are neither read nor multiplied and the DIF stages skip them
-    const int nz = NW_PRUNE ? wnz[fi] : E;
+    const int nz = NW_PRUNE ? max(1, wnz[fi] >> WSH) : E;
     // LDS-DMA only the X bins the pruned pass 0 reads: variant NZ (>= 4) reads bins < NZ*T,
     // i.e. NZ/2 rounds of 2*T bins, when it reads no mirrored bin (NZ <= E/2)
     const int nzv = nz < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz;
@@ -636,7 +640,7 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
 #ifndef NW_PAIR_PSUM
 #define NW_PAIR_PSUM 1
 #endif
-template <typename T, int N, int E, int OUT>
+template <typename T, int N, int E, int OUT, int WSH>
 hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* partials, int64_t nsig, hipStream_t s) {
     constexpr int threads = N / E;
     constexpr int kTileF = kTileFT<T>, kTileG = kTileGT<T>;
@@ -644,8 +648,8 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
-    e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, OUT, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            lds);
+    e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, OUT, true, WSH>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     const int64_t nsg = (nsig + kGroup - 1) / kGroup;
     const int64_t nsg_pad = (nsg + 8 * kTileG - 1) / (8 * kTileG) * (8 * kTileG);
@@ -665,7 +669,7 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
             kGroup, (int)nsg_pad, wnz);
         return hipGetLastError();
     }
-    nw_fused_kernel<T, N, E, OUT, true><<<blocks, threads, lds, s>>>(
+    nw_fused_kernel<T, N, E, OUT, true, WSH><<<blocks, threads, lds, s>>>(
         d, reinterpret_cast<const cplx<T>*>(X), wtab, partials, reinterpret_cast<const C2<T>*>(tw), nsig, kGroup,
         (int)nsg_pad, wnz);
     return hipGetLastError();
@@ -781,20 +785,31 @@ hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
     return hipGetLastError();
 }
 
-// epoch power partials: fp32, analytic rows, E <= 16 (W and the accumulators in registers)
+// epoch power / phase partials: analytic rows; fp32 power to E = 32, fp32 phases and fp64 at E = 16
 #ifndef NW_FUSED_PSUM
 #define NW_FUSED_PSUM 1
 #endif
 #ifndef NW_PSUM_MAXE
 #define NW_PSUM_MAXE 32   // power partials up to E = 32 (N = 8192, 16384)
 #endif
-template <typename T, int N, int E>
-constexpr bool kPSumOK = NW_FUSED_PSUM && std::is_same<T, float>::value && E <= NW_PSUM_MAXE;
-template <typename T, int N, int E>
-constexpr bool kPhSumOK = NW_FUSED_PSUM && std::is_same<T, float>::value && E <= 16;
+// Elements per thread of the partial-sum kernels (EO: the output kernels'): fp32 power keeps
+// EO (E = 32 at n = 8192 / 16384: E fp64 accumulators at 2 waves/SIMD); fp32 phases (2E fp64
+// accumulators) and fp64 (the drop-in's default dtype, 2 waves/SIMD already at 256 VGPRs)
+// run at E = 16 -- n = 8192 / 16384 then take 512 / 1024 threads, the W-support table
+// shifted by log2(EO / 16) (nw_fused_kernel's WSH)
+template <typename T, int EO, bool PHASE>
+constexpr int kPsE = (EO >= 32 && (PHASE || sizeof(T) == 8)) ? 16 : EO;
+template <int EO, int E> constexpr int kPsShift = EO == E ? 0 : EO == 2 * E ? 1 : 2;
+// combinations whose accumulators fit without spilling (tools/regs.py): at 1024 threads
+// (n = 16384, E = 16) a wave has 128 VGPRs, and neither fp64 power (228 B of scratch) nor
+// phases (fp32: 84 B) fit there -- n = 16384 keeps the chunk path for those
+template <typename T, int N, int EO>
+constexpr bool kPSumOK = NW_FUSED_PSUM && !(sizeof(T) == 8 && N / kPsE<T, EO, false> > 512);
+template <typename T, int N, int EO>
+constexpr bool kPhSumOK = NW_FUSED_PSUM && N / kPsE<T, EO, true> <= 512;
 
 bool fused_psum_supported(int64_t n, int dtype, int kind, bool phase) {
-    if (kind == NW_TABLE || dtype != NW_F32) return false;
+    if (kind == NW_TABLE) return false;
 #define NW_PS(TY, NN, EE) \
     if (n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) return phase ? kPhSumOK<TY, NN, EE> : kPSumOK<TY, NN, EE>;
     NW_FUSED_TABLE(NW_PS)
@@ -818,10 +833,12 @@ hipError_t fused_power_partials(const WDesc& d, int dtype, bool phase, const voi
 #define NW_PSL(TY, NN, EE)                                                                                    \
     if (d.n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) {                                          \
         if constexpr (kPhSumOK<TY, NN, EE>) {                                                                 \
-            if (phase) return launch_psum<TY, NN, EE, kOutPhSum>(d, X, wtab, partials, nsig, s);              \
+            constexpr int PE = kPsE<TY, EE, true>;                                                            \
+            if (phase) return launch_psum<TY, NN, PE, kOutPhSum, kPsShift<EE, PE>>(d, X, wtab, partials, nsig, s); \
         }                                                                                                     \
         if constexpr (kPSumOK<TY, NN, EE>) {                                                                  \
-            if (!phase) return launch_psum<TY, NN, EE, kOutPSum>(d, X, wtab, partials, nsig, s);              \
+            constexpr int PE = kPsE<TY, EE, false>;                                                           \
+            if (!phase) return launch_psum<TY, NN, PE, kOutPSum, kPsShift<EE, PE>>(d, X, wtab, partials, nsig, s); \
         }                                                                                                     \
         return hipErrorNotSupported;                                                                          \
     }

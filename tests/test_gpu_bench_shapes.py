@@ -183,7 +183,7 @@ def test_power_mean_fused_partials(n):
     assert max_err(pm[::51], orc.mean(axis=0)) <= 2e-5
 
 
-@pytest.mark.parametrize('n', [1024, 4096])
+@pytest.mark.parametrize('n', [1024, 4096, 8192])
 def test_itc_fused_partials(n):
     """ITC (mneutils.py:62-71) at the fused sizes: the kernel sums y / |y| (fp64, k_accumulate's
     formula) over each block of 8 signals.  Against the reference formula on the same plan's
@@ -209,3 +209,37 @@ def test_itc_fused_partials(n):
     err_fused = np.max(np.abs(itc[::51] - ref))
     err_mat = np.max(np.abs(np.abs(np.mean(c[:, ::51] / np.abs(c[:, ::51]), axis=0)) - ref))
     assert err_fused <= 2 * err_mat + 1e-6 and err_fused <= 1e-4, (err_fused, err_mat)
+
+
+@pytest.mark.parametrize('n', [1024, 2048, 4096, 8192, 16384])
+def test_fp64_fused_epoch_partials(n):
+    """fp64 (the drop-in's default dtype, the reference's complex128) epoch reductions
+    (mneutils.py:42-71): the kernel sums |y|^2 (ITC: y / hypot(y), the accumulator's formula)
+    over each block of 8 signals in fp64 -- at n <= 4096 on the output kernel's E = 16, at
+    n = 8192 on an E = 16 instantiation beside the E = 32 output kernel; n = 16384 keeps the
+    chunk path.  power_sum equals the sum of the same plan's per-signal power output (1e-13
+    where the same kernel computes both, else 1e-12); chunk-size independent; ITC against the
+    same plan's materialised cwt; both against the oracle (fp64 contract: 1e-12 of max, ITC
+    1e-10 absolute)."""
+    same = n <= 4096
+    S, freqs = 21, np.arange(1, 257, dtype=np.float64)
+    x = synth(S, n, seed=n + 5).astype(np.float64)
+    plan = plan_for(n, freqs, 'float64', 8)
+    pw = plan.execute(x, out_kind='power')
+    c = plan.execute(x, out_kind='cwt')
+    ps = plan.execute(x, out_kind='power_sum')
+    assert L.KERNEL_NAMES[plan.stats()['kernel']] == 'nw_fused_kernel'
+    np.testing.assert_allclose(ps, pw.sum(axis=0), rtol=1e-13 if same else 1e-12)
+    pm = plan.execute(x, out_kind='power_mean')
+    assert pm.dtype == np.float64 and pm.shape == (256, n)
+    np.testing.assert_allclose(pm, pw.mean(axis=0), rtol=1e-13 if same else 1e-12)
+    other = plan_for(n, freqs, 'float64', 3)                  # chunks 3, 3, ..., 3
+    np.testing.assert_allclose(other.execute(x, out_kind='power_sum'), ps, rtol=1e-13)
+    itc = plan.execute(x, out_kind='itc')
+    ref_itc = np.abs(np.mean(c / np.abs(c), axis=0))
+    assert np.max(np.abs(itc - ref_itc)) <= (1e-13 if same else 1e-10)
+    ph = other.execute(x, out_kind='phase_sum')
+    np.testing.assert_allclose(ph, plan.execute(x, out_kind='phase_sum'), rtol=1e-13, atol=1e-13 * S)
+    o = np.stack([O.cwt('morse', x[s], freqs[::51]) for s in range(S)])
+    assert max_err(pm[::51], np.mean(np.abs(o) ** 2, axis=0)) <= 1e-12
+    assert np.max(np.abs(itc[::51] - np.abs(np.mean(o / np.abs(o), axis=0)))) <= 1e-10

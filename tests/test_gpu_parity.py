@@ -118,7 +118,18 @@ def test_epochs_wavelet(kind, dtype):
     p = nw.EpochsWavelet(ep, CLASSES[kind](1000, dtype=dtype)).power('c', list(g['freqs']))
     assert rel_err(p, g['power_c']) <= 2 * t
     itc = nw.EpochsWavelet(ep, CLASSES[kind](1000, dtype=dtype)).itc('a', list(g['freqs']))
-    assert rel_err(itc, g['itc_a']) <= (1e-10 if dtype == 'float64' else 1e-3)
+    # ITC is a mean of unit phasors (values in [0, 1]): the contract is absolute.
+    # fp64: 1e-10.  fp32: 2e-5 where every epoch's |cwt| >= 0.1 x its scale row's max (the
+    # phase of y is then set to ~1e-6 by y's fp32 error); 1e-3 everywhere (near |y| = 0 the
+    # fp32 phase is arbitrary and moves the mean by up to 2/E per such epoch)
+    if dtype == 'float64':
+        assert np.max(np.abs(itc - g['itc_a'])) <= 1e-10
+    else:
+        ca = np.abs(nw.EpochsWavelet(ep, CLASSES[kind](1000, dtype='float64')).cwt('a', list(g['freqs'])))
+        good = ca.min(axis=0) >= 0.1 * ca.max(axis=(0, 2))[:, None]
+        assert good.sum() > 0.2 * good.size
+        err = np.abs(itc - g['itc_a'])
+        assert np.max(err[good]) <= 2e-5 and np.max(err) <= 1e-3, (np.max(err[good]), np.max(err))
 
 
 # ------------------------------------------------------------------ larger sizes
