@@ -188,7 +188,8 @@ def test_itc_fused_partials(n):
     """ITC (mneutils.py:62-71) at the fused sizes: the kernel sums y / |y| (fp64, k_accumulate's
     formula) over each block of 8 signals.  Against the reference formula on the same plan's
     cwt output, which runs on the pair kernel (its own fp32 rounding of y; the phase of a small
-    |y| amplifies it: 1e-5), chunk-size independent (phase_sum 1e-13), against the oracle (within
+    |y| amplifies it: 1e-5; 5e-5 at n = 8192, where the partials run at E = 16 and the cwt at
+    E = 32), chunk-size independent (phase_sum 1e-13), against the oracle (within
     2x the materialised cwt's own ITC error)."""
     S, freqs = 21, np.arange(1, 257, dtype=np.float64)
     x = synth(S, n, seed=n + 11)
@@ -197,7 +198,9 @@ def test_itc_fused_partials(n):
     itc = plan.execute(x, out_kind='itc')
     assert L.KERNEL_NAMES[plan.stats()['kernel']] == 'nw_fused_kernel'
     assert itc.shape == (256, n) and itc.dtype == np.float32
-    assert np.max(np.abs(itc - np.abs(np.mean(c / np.abs(c), axis=0)))) <= 1e-5
+    # n = 8192: the partials run at E = 16 beside the E = 32 cwt kernel (another fp32
+    # rounding of y, amplified by the phase of a small |y|)
+    assert np.max(np.abs(itc - np.abs(np.mean(c / np.abs(c), axis=0)))) <= (1e-5 if n <= 4096 else 5e-5)
     ph = plan.execute(x, out_kind='phase_sum')
     assert ph.dtype == np.complex128
     other = plan_for(n, freqs, 'float32', 3)

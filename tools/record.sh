@@ -1,10 +1,11 @@
 #!/bin/bash
-# Round-2 measurement record on the final build: GPU tests, smoke, bench lines, rocprofv3
+# Measurement record of the current build: GPU tests, smoke, bench lines, rocprofv3
 # kernel-trace --stats and PMC passes (traffic tied to the engine-source hash) for C4, C3,
-# C5 and the fp64 C4 shape.  Output under gpurun_out/rec/; stops at the first failure.
+# C5 and the fp64 C4 shape.  Output under $REC (default gpurun_out/rec/); stops at the first
+# failure; tools/collect.sh copies it into profiles/.  CFGS selects configs, SKIP_TESTS=1 the tests.
 set -u
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
-R=gpurun_out/rec; mkdir -p $R
+R=${REC:-gpurun_out/rec}; mkdir -p $R
 if [ -z "${SKIP_TESTS:-}" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $R/pytest_gpu.log 2>&1; rc=$?; tail -2 $R/pytest_gpu.log; [ $rc -ne 0 ] && exit $rc
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $R/smoke.log 2>&1; rc=$?; tail -1 $R/smoke.log; [ $rc -ne 0 ] && exit $rc
@@ -25,10 +26,10 @@ record() {
 CFGS=${CFGS:-c4 c3 c5 c4f64}
 for c in $CFGS; do
   case $c in
-    c4) record c4 "--steps 10 --warmup 3" "--config c4 --steps 2 --warmup 1" "nw_fused_kernel" '{"chunk": 512, "n": 16384, "freqs": 256, "out": "cwt", "dtype": "float32"}' || exit $? ;;
+    c4) record c4 "--steps 10 --warmup 3" "--config c4 --steps 2 --warmup 1 --no-fp64" "nw_fused_kernel" '{"chunk": 512, "n": 16384, "freqs": 256, "out": "cwt", "dtype": "float32"}' || exit $? ;;
     c3) record c3 "--config c3 --steps 5 --warmup 2" "--config c3 --steps 2 --warmup 1" "nw_fused_pair_kernel" '{"chunk": 1024, "n": 4096, "freqs": 256, "out": "power", "dtype": "float32"}' || exit $? ;;
     c5) record c5 "--config c5 --steps 3 --warmup 1" "--config c5 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float32", "scales_per_launch": 16}' || exit $? ;;
-    c4f64) record c4f64 "--config c4 --dtype float64 --epochs 64 --steps 3 --warmup 1" "--config c4 --dtype float64 --epochs 16 --steps 2 --warmup 1" "nw_fused_kernel" '{"chunk": 512, "n": 16384, "freqs": 256, "out": "cwt", "dtype": "float64"}' || exit $? ;;
+    c4f64) record c4f64 "--config c4 --dtype float64 --steps 3 --warmup 1" "--config c4 --dtype float64 --epochs 16 --steps 2 --warmup 1" "nw_fused_kernel" '{"chunk": 512, "n": 16384, "freqs": 256, "out": "cwt", "dtype": "float64"}' || exit $? ;;
   esac
 done
 exit 0
