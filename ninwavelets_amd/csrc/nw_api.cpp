@@ -295,9 +295,6 @@ int run_fft_rows(nw_plan* p, bool inverse, int64_t rows, char* in, char* out, si
 // The chirp-z table (W rows, supports, rows grouped by M) of the current wavelet.  A
 // tentative length (2n - 1 > M_max) whose rows do not all fit switches the plan to the
 // rocFFT engine until the next nw_plan_set_wavelet.
-#ifndef NW_CHIRP_HYBRID
-#define NW_CHIRP_HYBRID 1   // wide rows of a tentative length to rocFFT, the rest on chip
-#endif
 
 // The compacted view of the rows `rows` of the current desc (device arrays gathered on the
 // device): per-row freq / peak / xstep32 / row_len and table rows, plus the scatter map
@@ -363,7 +360,7 @@ int chirp_table(nw_plan* p) {
     if (!fits) {
         if (!p->chirp_tentative)
             return fail(NW_E_INVALID, "chirp-z form: a wavelet row is wider than the largest on-chip transform");
-        if (!NW_CHIRP_HYBRID || (int)over.size() >= p->nfreq) {   // no row fits: the rocFFT engine
+        if ((int)over.size() >= p->nfreq) {   // no row fits: the rocFFT engine
             p->chirp = false;
             p->engine = NW_ENGINE_ROCFFT;
             p->stats.engine = NW_ENGINE_ROCFFT;
@@ -412,22 +409,13 @@ int run_overflow_rows(nw_plan* p, int64_t c, void* dst, int out_kind) {
     });
 }
 
-#ifndef NW_OWN_FORWARD
-#define NW_OWN_FORWARD 1   // fused sizes: forward R2C by nw_fused.hip's fwd_r2c_kernel (no copy, one kernel)
-#endif
-
-#ifndef NW_REDUCE_PSUM
-#define NW_REDUCE_PSUM 1   // epoch power sums: fused per-block partials (nw::fused_power_partials)
-#endif
-#ifndef NW_REDUCE_PHSUM
-#define NW_REDUCE_PHSUM 1   // epoch phase sums (ITC): the same with y / |y|
-#endif
 constexpr int OUT_PSUM = 1001;    // internal run_chunk kinds: (ceil(c / 8), F, n) fp64 power partials,
 constexpr int OUT_PHSUM = 1002;   // complex fp64 phase partials (y / |y|)
 
 int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
-    if (NW_OWN_FORWARD && !rocfft_engine && !p->large && !p->chirp) {
+    // fused sizes: the forward R2C by nw_fused.hip's fwd_r2c_kernel (no copy, one kernel)
+    if (!rocfft_engine && !p->large && !p->chirp) {
         // power-of-two n <= 16384: the on-chip forward transform reads the caller's rows directly
         NW_TRY(staged(p, ST_FWD, [&] {
             NW_HIP(nw::fused_forward(p->n, p->dtype, xs_dev, p->d_X, c, p->nh, p->stream));
@@ -606,7 +594,7 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     // over each block of 8 signals in fp64, the accumulator adds the ceil(c / 8) fp64 partials
     // (the same fp64 additions of the same fp32-derived values, regrouped; with the dedup view
     // the partials of the distinct rows are expanded like any output row)
-    const bool psum = fused && !p->large && !p->chirp && (phase ? NW_REDUCE_PHSUM : NW_REDUCE_PSUM) &&
+    const bool psum = fused && !p->large && !p->chirp &&
                       nw::fused_psum_supported(p->n, p->dtype, p->desc.kind, phase);
     const int sig_kind = psum ? (phase ? OUT_PHSUM : OUT_PSUM) : (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
     // partials: plain fp64 sums (phase partials as 2 fn reals)
@@ -663,9 +651,7 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
 
 // ---- host-buffer copy-out: pinned double-buffered pieces + a multi-threaded host copy
 constexpr size_t kPiece = size_t(64) << 20;
-#ifndef NW_COPY_THREADS
-#define NW_COPY_THREADS 8
-#endif
+constexpr int kCopyThreads = 8;
 
 int copy_out(nw_plan* p, char* dst, const char* src, size_t bytes) {
     if (!p->pinned[0]) {
@@ -686,7 +672,7 @@ int copy_out(nw_plan* p, char* dst, const char* src, size_t bytes) {
             const size_t k = i - 1, off = k * kPiece;
             NW_HIP(hipEventSynchronize(p->pinned_ev[k & 1]));
             nw::host::parallel_copy(dst + off, (const char*)p->pinned[k & 1], std::min(kPiece, bytes - off),
-                                   NW_COPY_THREADS);
+                                   kCopyThreads);
         }
     }
     return NW_OK;

@@ -25,10 +25,8 @@
 namespace nw {
 namespace {
 
-#ifndef NW_CHIRP_GROUP
-#define NW_CHIRP_GROUP 8   // measured (n = 1201 / 4097): 4 -2 % / -1 %, 16 +0.6 % / +0.6 % (noise)
-#endif
-constexpr int kGroupC = NW_CHIRP_GROUP;   // signals per block
+// signals per block; measured (n = 1201 / 4097): 4 -2 % / -1 %, 16 +0.6 % / +0.6 % (noise)
+constexpr int kGroupC = 8;
 constexpr int kTileFC = 8;    // scales per XCD tile
 constexpr int kTileGC = 4;    // signal groups per XCD tile
 constexpr int kRegOsz = 16;   // PassInfo without last-pass pairing: j = t + q*T everywhere
@@ -83,23 +81,8 @@ __device__ __forceinline__ C2<T> chirp(int k, uint32_t n2, float inv_n2, const C
     }
 }
 
-// fp32 chirp from an exact phase index m = k^2 mod 2n (revolutions m / 2n)
-[[maybe_unused]] __device__ __forceinline__ C2<float> chirp_m(uint32_t m, float inv_n2) {
-    const float rev = (float)m * inv_n2;
-    return C2<float>{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
-}
-// (a + b) mod n for a, b < n: one add, one subtract, one unsigned min
-[[maybe_unused]] __device__ __forceinline__ uint32_t addmod(uint32_t a, uint32_t b, uint32_t n) {
-    const uint32_t s = a + b;
-    return min(s, s - n);
-}
-#ifndef NW_CHIRP_INC
-#define NW_CHIRP_INC 0   // fp32 phase indices k^2 mod 2n by exact modular increments instead of a urem
-                         // per element: measured 2.7 % slower (n = 1201 power and cwt), off
-#endif
-#ifndef NW_CHIRP_SKIP_EPI
-#define NW_CHIRP_SKIP_EPI 1   // |y| and |y|^2 skip the final chirp: |c(n) y'| = |y'|
-#endif
+// (fp32 phase indices k^2 mod 2n by exact modular increments instead of one urem per
+// element measured 2.7 % slower at n = 1201, power and cwt: not kept)
 
 template <typename T, bool REALW> struct WRow;
 template <typename T> struct WRow<T, true> {
@@ -114,11 +97,8 @@ template <typename T> struct WRow<T, false> {
 // waves per SIMD without scratch (tools/regs.py): fp32 M <= 4096 fit 168 VGPRs (3 waves;
 // 4 spilled 44 B at M = 1024), M >= 8192 and fp64 need up to 256 (2 waves; fp32 M = 16384
 // at E = 32 still spills ~230 B there)
-#ifndef NW_CHIRP_WPS8192
-#define NW_CHIRP_WPS8192 2
-#endif
 template <typename T, int M, int E>
-constexpr int kChirpWps = E <= 8 ? 4 : (sizeof(T) == 4 && M <= 4096 && E <= 16) ? 3 : (sizeof(T) == 4 && M == 8192 && E <= 16) ? NW_CHIRP_WPS8192 : 2;
+constexpr int kChirpWps = E <= 8 ? 4 : (sizeof(T) == 4 && M <= 4096 && E <= 16) ? 3 : 2;
 template <typename T, int M, int E, int OUT, bool REALW>
 __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     WDesc d, const cplx<T>* __restrict__ X, const void* __restrict__ wtab, void* __restrict__ out,
@@ -153,11 +133,6 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
     const float inv_n2 = 1.0f / (float)n2;
     const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * n;
     const int nz = (ksup[fi] + TT - 1) / TT;   // pass-0 elements reaching the support (<= E/2)
-    // fp32 phase index of k = t + r*T: m_r = k^2 mod 2n, m_{r+1} = m_r + s_r, s_r = (2 T k + T^2)
-    // mod 2n, s_{r+1} = s_r + 2 T^2 (all mod 2n; exact, t < T <= 1024)
-    const uint32_t mk0 = ((uint32_t)t * (uint32_t)t) % n2;
-    const uint32_t sk0 = (2u * TT * (uint32_t)t + (uint32_t)TT * TT) % n2;
-    const uint32_t dk = (2u * TT * TT) % n2;
     Tab1<T, M, E>::fill(lds, tw, t);
     for (int64_t s = s_begin; s < s_end; ++s) {
         const cplx<T>* Xs = X + s * d.nh;
@@ -166,22 +141,15 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
         // only the elements r < NZ (bins k < NZ*T) can meet the row's support K <= M/2: the
         // others are zero for every thread and the DIF stages skip them (as nw_fused's pass 0)
         auto pass0 = [&]<int NZ>() {
-            uint32_t mk = mk0, sk = sk0;
-            asm volatile("" : "+v"(mk), "+v"(sk));   // per row: not hoisted as NZ live values
 #pragma unroll
             for (int r = 0; r < E; ++r) {
                 const int k = t + r * TT;
                 C2<T> a{T(0), T(0)};
                 if (r < NZ && k < n) {
                     const C2<T> z = WRow<T, REALW>::apply(wrow[k], spectrum_bin<T>(Xs, d, k));
-                    if constexpr (sizeof(T) == 4 && NW_CHIRP_INC) a = cmul(z, chirp_m(mk, inv_n2));
-                    else a = cmul(z, chirp<T>(k, n2, inv_n2, ct));
+                    a = cmul(z, chirp<T>(k, n2, inv_n2, ct));
                 }
                 v[r] = C2<T>{a.re, -a.im};
-                if (r + 1 < NZ) {
-                    mk = addmod(mk, sk, n2);
-                    sk = addmod(sk, dk, n2);
-                }
             }
             idft_br<T, E, NZ>(v);
         };
@@ -214,32 +182,17 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
         O* orow = reinterpret_cast<O*>(out) + (s * d.nfreq + fi) * (int64_t)n;
 #pragma unroll
         for (int q = 0; q < IL::Q; ++q) {
-            // outputs n_j = n0 + j*NS in natural j order (register i = bitrev(j)); fp32 phase
-            // indices by modular increments from n0^2 mod 2n
+            // outputs n_j = n0 + j*NS in natural j order (register i = bitrev(j)); |y| and
+            // |y|^2 skip the final chirp (|c(n) y'| = |y'|: n = 1201 power 1.397 -> 1.313 ms)
             const uint32_t n0 = (uint32_t)(t + q * TT);
-            uint32_t mn = 0, sn = 0, dn = 0;
-            constexpr bool EPI = OUT == NW_OUT_CWT || !NW_CHIRP_SKIP_EPI;
-            if constexpr (EPI && sizeof(T) == 4 && NW_CHIRP_INC) {
-                mn = (n0 * n0) % n2;
-                sn = (2u * n0 * (uint32_t)IL::NS + (uint32_t)IL::NS * IL::NS) % n2;
-                dn = (2u * (uint32_t)IL::NS * IL::NS) % n2;
-            }
+            constexpr bool EPI = OUT == NW_OUT_CWT;
 #pragma unroll
             for (int j = 0; j < IL::R; ++j) {
                 const int i = bitrev<IL::R>(j);
                 const int idx = (int)n0 + j * IL::NS;
                 C2<T> y = v[q * IL::R + i];
-                if constexpr (EPI) {
-                    if constexpr (sizeof(T) == 4 && NW_CHIRP_INC) y = cmul(y, chirp_m(mn, inv_n2));
-                    else y = cmul(y, chirp<T>(idx, n2, inv_n2, ct));
-                }
+                if constexpr (EPI) y = cmul(y, chirp<T>(idx, n2, inv_n2, ct));
                 if (idx < n) orow[idx] = out_value<OUT, T>(y);
-                if constexpr (EPI && sizeof(T) == 4 && NW_CHIRP_INC) {
-                    if (j + 1 < IL::R) {
-                        mn = addmod(mn, sn, n2);
-                        sn = addmod(sn, dn, n2);
-                    }
-                }
             }
         }
     }
@@ -402,20 +355,10 @@ hipError_t launch_m_e(const WDesc& d, int out_kind, const void* X, const void* w
 // fp32 M = 8192: |y| and |y|^2 at E = 32 (256 threads, two blocks per CU, 3 passes, no
 // scratch): measured N = 4097 power 10.60 -> 8.75 ms, N = 3001 6.60 -> 5.82 ms per launch;
 // the complex output spills at E = 32 (108-128 B) and keeps E = 16
-#ifndef NW_CHIRP_E8192_POW
-#define NW_CHIRP_E8192_POW 32
-#endif
-#ifndef NW_CHIRP_E4096_POW
-#define NW_CHIRP_E4096_POW 16
-#endif
-#ifndef NW_CHIRP_E2048_POW
-#define NW_CHIRP_E2048_POW 16
-#endif
 template <typename T, int M, int E, bool REALW>
 hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
                     const int* rowmap, int nrows, const int* ksup, hipStream_t s) {
-    constexpr int EP = sizeof(T) != 4 ? E : M == 8192 ? NW_CHIRP_E8192_POW : M == 4096 ? NW_CHIRP_E4096_POW
-                                            : M == 2048 ? NW_CHIRP_E2048_POW : E;
+    constexpr int EP = (sizeof(T) == 4 && M == 8192) ? 32 : E;
     if constexpr (EP != E) {
         if (out_kind != NW_OUT_CWT)
             return launch_m_e<T, M, EP, REALW>(d, out_kind, X, wtab, out, nsig, rowmap, nrows, ksup, s);
@@ -426,15 +369,8 @@ hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wta
 }  // namespace
 
 // (dtype, M, E) of the chirp engine: fp32 M <= 16384 (E = 32 at 16384), fp64 M <= 8192
-#ifndef NW_CHIRP_E
-#define NW_CHIRP_E 16   // elements per thread, fp32 M <= 8192
-#endif
-#ifndef NW_CHIRP_E8192
-#define NW_CHIRP_E8192 NW_CHIRP_E
-#endif
 #define NW_CHIRP_TABLE(X)                                                                        \
-    X(float, 1024, NW_CHIRP_E) X(float, 2048, NW_CHIRP_E) X(float, 4096, NW_CHIRP_E)             \
-    X(float, 8192, NW_CHIRP_E8192) X(float, 16384, 32)                                           \
+    X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, 16) X(float, 8192, 16) X(float, 16384, 32) \
     X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) X(double, 8192, 16)
 
 int64_t chirp_mmax(int dtype) { return dtype == NW_F32 ? 16384 : 8192; }

@@ -9,33 +9,19 @@
 
 #include "nw_internal.h"
 
-#ifndef NW_HWTWIDDLE
-#define NW_HWTWIDDLE 1   // fp32 twiddles from v_cos/v_sin (no loads); fp64 always uses the table
-#endif
-#ifndef NW_PACK_STORES
-#define NW_PACK_STORES 1   // unpaired last pass: lane-pair transposes -> 16-B stores
-#endif
-#ifndef NW_PACK_MAX
-#define NW_PACK_MAX 2      // measured (n = 4096): pairs of 8-B outputs 0.413 -> 0.403 ms (cwt);
-                           // quads of 4-B outputs 0.337 -> 0.360 ms (power), pairs of them (8-B
-                           // stores) C3 1.253 -> 1.277 ms (round 3): slower, so 8-B outputs only
-#endif
-
-#ifndef NW_PRUNE
-#define NW_PRUNE 1         // pass 0 skips the elements beyond the W row's support
-#endif
-#ifndef NW_PRUNE_MIN
-#define NW_PRUNE_MIN 4     // smallest pass-0 variant (support rounded up to it; 1 and 2 add
-                           // code without a measurable gain)
-#endif
-#ifndef NW_SWZ_LAST
-#define NW_SWZ_LAST 1      // conflict-free paired last-pass reads at T = 512 (PassInfo::SWZ)
-#endif
-#ifndef NW_XDMA_MIN_E
-#define NW_XDMA_MIN_E 32 // fp32 with E >= this: the next signal's X copied into the idle LDS
-                         // image by LDS-DMA before the stores (measured: E=32 1.99 -> 1.94 ms,
-                         // E=16 0.362 -> 0.386 ms, so off there)
-#endif
+// Tuning constants; each was measured against its alternatives (numbers in DESIGN.md §4).
+// unpaired last pass: lane-pair transposes (DPP) regroup outputs of <= 8 B into 16-B stores
+// (pairs of 8-B outputs: n = 4096 cwt 0.413 -> 0.403 ms); 4-B outputs stay single stores
+// (quads: 0.337 -> 0.360 ms at n = 4096 power, pairs: C3 1.253 -> 1.277 ms)
+constexpr int kPackMax = 2;
+// smallest pass-0 variant: a W row's support is rounded up to it (1 and 2 add code without a
+// measurable gain)
+constexpr int kPruneMin = 4;
+// fp32 kernels with E >= this take the next signal's X by LDS-DMA into the idle image before
+// the stores (E = 32: 1.99 -> 1.94 ms; E = 16: 0.362 -> 0.386 ms, so not there)
+constexpr int kXdmaMinE = 32;
+// W held in registers for the whole block when E <= this
+constexpr int kWregMaxE = 16;
 
 
 namespace nw {
@@ -53,12 +39,6 @@ typedef float f2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ C2<f2> pk(C2<float> a, C2<float> b) { return {f2{a.re, b.re}, f2{a.im, b.im}}; }
 __device__ __forceinline__ C2<float> lo(C2<f2> p) { return {p.re.x, p.im.x}; }
 __device__ __forceinline__ C2<float> hi(C2<f2> p) { return {p.re.y, p.im.y}; }
-#ifndef NW_PK
-#define NW_PK 1   // packed fp32 math for pairs of butterflies (Q >= 2 passes)
-#endif
-#ifndef NW_TW_PAIR
-#define NW_TW_PAIR 1   // paired last pass: second butterfly's twiddle bases from the first's
-#endif
 
 // a rounded product that the compiler may not fuse into a following add
 __device__ __forceinline__ double mul_nocontract(double a, double b) {
@@ -198,7 +178,7 @@ __device__ __forceinline__ void twiddle_bases(C2<T>* p, int m, const C2<T>* __re
             // w_N^i = hi[i >> 5] * lo[i & 31] from the LDS split table (TwSplit), i < N/2
             const uint32_t i = ((uint32_t)m << k) * (uint32_t)(N / NSR);
             p[k] = cmul(split[i >> 5], split[N / 64 + (i & 31)]);
-        } else if constexpr (sizeof(T) == 4 && NW_HWTWIDDLE) {
+        } else if constexpr (sizeof(T) == 4) {
             // v_cos/v_sin take revolutions; (m << k) / NSR is exact in fp32 (power-of-two
             // denominator), measured max abs error 1.2e-7 over all 16384 angles: no memory
             // access, so nothing queues behind this wave's in-flight stores
@@ -259,25 +239,14 @@ template <int N, int E> struct Geometry {
     }
 };
 
-// The image feeding pass P may use its own padding group PG (slots of 2 pad slots).
-// Signal-pair kernel at T = 256 (n = 4096, E = 16): pass 0 writes each lane's 16 slots as
-// 8 ds_write_b128 of 16 B; with 2 pad slots per 32 two lanes share a pad block, so lanes
-// t, t+1 of every 8-lane group hit the same banks (2-way on every pass-0 write,
-// SQ_LDS_BANK_CONFLICT 0.54 of LDS cycles at C3).  Padding the 0 -> 1 image per 16 slots
-// makes those writes conflict-free (stride 18 slots = 36 dwords per lane); pass 1's
-// lanes 16-31 of each 32-lane ds_read_b64 group then take the butterfly block 8 blocks
-// further (PassInfo::REMAP: 8 * 18 slots = 288 = 32 mod 64 dwords), so those reads stay
-// conflict-free too.  The 1 -> 2 image keeps 2 per 32 (its accesses are lane-contiguous).
-#ifndef NW_PAIR_PAD16
-#define NW_PAIR_PAD16 0   // conflict-free, but measured 1.4 % slower at C3 (1.234 -> 1.252 ms per launch): off
-#endif
+// The image feeding pass P and its padding group (2 pad slots per kPadG<E> slots).  (A
+// per-16 padding of the signal-pair kernel's 0 -> 1 image at n = 4096 removed its 2-way
+// pass-0 write conflicts, 0.54 of LDS cycles at C3, but measured 1.4 % slower: not kept.)
 template <int PG> __device__ __forceinline__ int lds_idx_p(int i) { return i + 2 * (i / PG); }
 template <int PG> constexpr int lds_off_p(int c) { return c + 2 * (c / PG); }
 template <typename T> constexpr bool kIsPair = !std::is_same<T, Sc<T>>::value;
-template <typename T, int N, int E>
-constexpr bool kPad16 = NW_PAIR_PAD16 && kIsPair<T> && E == 16 && N / E == 256 && Geometry<N, E>::npass() > 2;
-template <typename T, int N, int E, int P> constexpr int kPadX = (kPad16<T, N, E> && P == 1) ? 16 : kPadG<E>;
-template <typename T, int N, int E> constexpr int kImgElems = kPad16<T, N, E> ? N + 2 * (N / 16) : lds_elems<N, E>();
+template <typename T, int N, int E, int P> constexpr int kPadX = kPadG<E>;
+template <typename T, int N, int E> constexpr int kImgElems = lds_elems<N, E>();
 
 // output value of one point: y, |y| or |y|^2
 template <int OUT, typename T> struct OutT { using type = T; };
@@ -290,9 +259,6 @@ constexpr int kOutXHalf = 1000;
 constexpr int kOutPSum = 1001;
 // ... and the phase sums of ITC: acc[2e], acc[2e + 1] += y / |y| in fp64
 constexpr int kOutPhSum = 1002;
-#ifndef NW_PHSUM_RSQ
-#define NW_PHSUM_RSQ 1
-#endif
 struct alignas(16) XHalfSlot { double a, b; };
 template <typename T> struct OutT<kOutXHalf, T> { using type = XHalfSlot; };
 template <int OUT, typename T>
@@ -305,6 +271,7 @@ __device__ __forceinline__ typename OutT<OUT, T>::type out_value(C2<T> y) {
 // store outputs idx, idx+1 of the current row (orow: wave-uniform row base) as ONE
 // vector store (16 B for complex64, 8 B for float32, 2x16 B for complex128)
 // outputs lane_idx + c_idx (pair: and the next one) of the current row
+// streaming (nt) stores: measured 5 % faster than plain at n = 16384
 template <int OUT, typename T>
 __device__ __forceinline__ void store_pair(void* orow, uint32_t lane_idx, uint32_t c_idx, C2<T> y0, C2<T> y1) {
     using O = typename OutT<OUT, T>::type;
@@ -313,7 +280,6 @@ __device__ __forceinline__ void store_pair(void* orow, uint32_t lane_idx, uint32
     asm volatile("" ::"v"(y0.re), "v"(y0.im), "v"(y1.re), "v"(y1.im), "v"(lane_idx));
     return;
 #endif
-#ifndef NW_PLAIN_STORE   // streaming (nt) stores: measured 5 % faster than plain at n = 16384
     using V = typename std::conditional<sizeof(P2) == 16, float __attribute__((ext_vector_type(4))),
               typename std::conditional<sizeof(P2) == 8, float __attribute__((ext_vector_type(2))),
                                         double __attribute__((ext_vector_type(4)))>::type>::type;
@@ -321,10 +287,6 @@ __device__ __forceinline__ void store_pair(void* orow, uint32_t lane_idx, uint32
     __builtin_nontemporal_store(__builtin_bit_cast(V, pv),
                                 reinterpret_cast<V*>(at(reinterpret_cast<P2*>(orow), lane_idx * (uint32_t)sizeof(O),
                                                         c_idx * (uint32_t)sizeof(O))));
-#else
-    *at(reinterpret_cast<P2*>(orow), lane_idx * (uint32_t)sizeof(O), c_idx * (uint32_t)sizeof(O)) =
-        P2{out_value<OUT, T>(y0), out_value<OUT, T>(y1)};
-#endif
 }
 template <int OUT, typename T>
 __device__ __forceinline__ void store_one(void* orow, uint32_t lane_idx, uint32_t c_idx, C2<T> y) {
@@ -383,25 +345,6 @@ template <int N, int E, int P, int OSZ = 8, bool PK = false> struct PassInfo;
 template <typename T, int N, int E, int P, int COMP>
 __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
     using G = Geometry<N, E>;
-#ifdef NW_ABL_ADDTID
-    // diagnostic only (wrong results): the same bytes written as lane-contiguous
-    // ds_write_addtid_b32 (no address VGPR, 128 B/clk/CU) -- what cheaper exchange writes buy
-    {
-        constexpr int W = sizeof(T) / 4;
-#pragma unroll
-        for (int i = 0; i < E; ++i) {
-            T x = comp<COMP>(v[i]);
-            const uint32_t* d = reinterpret_cast<const uint32_t*>(&x);
-#pragma unroll
-            for (int k = 0; k < W; ++k)
-                asm volatile("s_mov_b32 m0, 0\n\tds_write_addtid_b32 %0 offset:%1" ::"v"(d[k]), "i"(((i * W + k) % 64) * 256)
-                             : "memory");   // m0 is reserved: the compiler re-sets it before its own uses
-        }
-        (void)lds;
-        (void)t;
-        return;
-    }
-#endif
     constexpr int PG = kPadX<T, N, E, P + 1>;
     if constexpr (P == 0) {
         Pair<T>* dst = reinterpret_cast<Pair<T>*>(lds + lds_idx_p<PG>(t * E));
@@ -447,11 +390,8 @@ template <int N, int E, int P, int OSZ, bool PK> struct PassInfo {
     // 16-31 of each group take the pair block 16 blocks further (512 slots: 16 * 34 =
     // 544 = 32 mod 64 dwords), so a group covers the 64 banks once.  Stores stay whole:
     // each store instruction writes two 512-B runs.
-    static constexpr bool SWZ = PAIRED && NW_SWZ_LAST && G::T == 512 && kPadG<E> == 32;
-    // signal-pair kernel, n = 4096: pass 1 reads the per-16-padded image (see kPad16)
-    static constexpr bool REMAP = PK && NW_PAIR_PAD16 && P == 1 && !LAST && E == 16 && G::T == 256 && Q == 1;
+    static constexpr bool SWZ = PAIRED && G::T == 512 && kPadG<E> == 32;
     __device__ static __forceinline__ int bfly(int t, int q) {
-        if constexpr (REMAP) return ((t >> 5) << 4) + (((t >> 4) & 1) << 7) + (t & 15);
         if constexpr (SWZ) return 2 * (((t >> 5) << 4) + (((t >> 4) & 1) << 8) + (t & 15)) + q;
         return PAIRED ? Q * t + q : t + q * G::T;
     }
@@ -461,12 +401,6 @@ template <int N, int E, int P, int OSZ, bool PK> struct PassInfo {
 // radix): an NS x (R-1) table in LDS after the image (7.75 KiB at n = 16384 fp32),
 // filled once per block from the exact global table, replaces that pass's v_sin/v_cos
 // bases and their products (the kernel is power-bound: every VALU op saved counts).
-#ifndef NW_TAB1
-#define NW_TAB1 1
-#endif
-#ifndef NW_TAB1_64
-#define NW_TAB1_64 0
-#endif
 template <typename T, int N, int E> struct Tab1 {
     using I = PassInfo<N, E, 1>;
     using S = Sc<T>;                                // entries in the scalar type (shared by a pair)
@@ -474,8 +408,9 @@ template <typename T, int N, int E> struct Tab1 {
     static constexpr int COUNT = Geometry<N, E>::npass() >= 2 ? NS * (R - 1) : 0;
     // fp64 at n = 16384: one block per CU whatever the table costs (256 VGPRs), and image +
     // table (155 KiB) fit the CU's LDS
-    static constexpr bool ON = NW_TAB1 && COUNT > 0 &&
-                               (COUNT * (int)sizeof(C2<S>) <= 8192 || (NW_TAB1_64 && sizeof(S) == 8 && N == 16384));
+    // (fp64 at n = 16384, 15.5 KiB beside the 136 KiB image, measured +2.5 % alone and
+    // slower than the X LDS-DMA it would share the space with: not kept)
+    static constexpr bool ON = COUNT > 0 && COUNT * (int)sizeof(C2<S>) <= 8192;
     static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<S>) : 0;
     static_assert((kImgElems<T, N, E> * sizeof(T)) % 16 == 0, "table alignment");
     __device__ static __forceinline__ const C2<S>* table(const T* lds) {
@@ -523,12 +458,8 @@ __device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
 // wait for ALL of the wave's in-flight global stores.  The exchanges only need
 // this wave's LDS operations complete (lgkmcnt(0)) before the s_barrier.
 __device__ __forceinline__ void lds_barrier() {
-#ifdef NW_FENCED_BARRIER
-    __syncthreads();
-#else
     __builtin_amdgcn_s_waitcnt(0xC07F);   // vmcnt(63) expcnt(7) lgkmcnt(0): LDS ops only
     __builtin_amdgcn_s_barrier();
-#endif
 }
 
 // ---- LDS-DMA of the next signal's half spectrum X[0 .. N/2) (N*4 bytes) into the idle
@@ -606,8 +537,7 @@ struct LastStores {
     static constexpr int R = I::R, Q = I::Q;
     static constexpr int STEP = I::PAIRED ? 2 : 1;
     static constexpr int PACK_W = (int)(16 / sizeof(O));
-    static constexpr int PACK = (!I::PAIRED && NW_PACK_STORES && PACK_W <= NW_PACK_MAX && R % PACK_W == 0)
-                                    ? PACK_W : 1;
+    static constexpr int PACK = (!I::PAIRED && PACK_W <= kPackMax && R % PACK_W == 0) ? PACK_W : 1;
     static_assert(PACK == 1 || PACK == 2 || PACK == 4, "pack");
     static constexpr int COUNT = PACK > 1 ? Q * R / PACK : Q / STEP * R;   // store instructions per thread per signal
     // all stores of one signal (v: the last pass's registers, bit-reversed rows)
@@ -674,40 +604,17 @@ struct LastStores {
 };
 
 
-#ifndef NW_WREG_MAX_E
-#define NW_WREG_MAX_E 16   // W held in registers for the block when E <= this
-#endif
 
-// complex W rows (tables) keep the register path: with LDS-DMA they exceed 128 VGPRs
-#ifndef NW_XDMA64
-#define NW_XDMA64 1   // fp64 E = 32 too: n = 16384 fp64 cwt 10.90 -> 9.88 ms per 512-signal launch (one box)
-#endif
-#ifndef NW_XDMA64_MIN_E
-#define NW_XDMA64_MIN_E 32
-#endif
+// LDS-DMA of the next signal's X: fp32 at E >= kXdmaMinE, fp64 at E = 32 (n = 16384 fp64 cwt
+// 10.90 -> 9.88 ms per 512-signal launch); analytic rows only (complex table rows keep the
+// register path: with LDS-DMA they exceed 128 VGPRs)
 template <typename T, int E, bool REALW>
-constexpr bool kXDMA = (sizeof(T) == 4 ? E >= NW_XDMA_MIN_E : (NW_XDMA64 && E >= NW_XDMA64_MIN_E)) && REALW;
+constexpr bool kXDMA = E >= (sizeof(T) == 4 ? kXdmaMinE : 32) && REALW;
 // DMA rounds (T lanes x 16 B each) holding the first nz pass-0 elements (T bins each)
 template <typename T> __device__ __forceinline__ int dma_rounds_for(int nz) {
     return (nz * (int)sizeof(C2<T>) + 15) / 16;
 }
 
-// E = 16 (n <= 8192): X gets its OWN LDS buffer after the image and the pass-1 table, so
-// the next signal's X is DMA'd right after this signal's pass 0 and has the whole signal
-// (exchanges, passes, stores) to land; with W in registers, pass 0 then waits on nothing
-// issued after a store.  (At n = 16384 the 64 KiB buffer would cost a workgroup per CU.)
-#ifndef NW_XBUF
-#define NW_XBUF 0   // measured slower (C3 0.337 -> 0.360 ms): the buffer costs workgroups per CU
-#endif
-template <typename T, int N, int E> struct XBuf {
-    static constexpr bool ON = NW_XBUF && E < 32 && E <= NW_WREG_MAX_E;
-    static constexpr int OFFSET = kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES;
-    static constexpr int BYTES = ON ? (N / 2) * (int)sizeof(C2<T>) : 0;
-    static_assert(OFFSET % 16 == 0, "DMA alignment");
-    __device__ static __forceinline__ C2<T>* at_lds(T* lds) {
-        return reinterpret_cast<C2<T>*>(reinterpret_cast<char*>(lds) + OFFSET);
-    }
-};
 // fp64 twiddle bases from a split table in LDS: w_N^i = hi[i >> 5] * lo[i & 31] for i < N/2,
 // N/64 + 32 exact entries (4.5 KiB at N = 16384) filled once per block from the exact global
 // table, so no base is a global load (a load issued after this wave's stores waits for all
@@ -716,16 +623,11 @@ template <typename T, int N, int E> struct XBuf {
 // Measured (one box, interleaved): fp64 N = 4096 1.950 -> 1.900 ms per launch (+2.7 %), but
 // N = 16384 (E = 32, X by LDS-DMA) 9.80 -> 10.0-10.3 ms and the C5 fp64 row pass 0.94 -> 0.95:
 // on for N <= 4096 only.
-#ifndef NW_TWSPLIT64
-#define NW_TWSPLIT64 1
-#endif
-#ifndef NW_TWSPLIT64_MAXN
-#define NW_TWSPLIT64_MAXN 4096
-#endif
 template <typename T, int N, int E> struct TwSplit {
-    static constexpr bool ON = NW_TWSPLIT64 && std::is_same<T, double>::value && N >= 2048 && N <= NW_TWSPLIT64_MAXN;
+    static constexpr bool ON = std::is_same<T, double>::value && N >= 2048 && N <= 4096;
     static constexpr int NHI = N / 64, COUNT = NHI + 32;
-    static constexpr int OFFSET = XBuf<T, N, E>::OFFSET + XBuf<T, N, E>::BYTES;
+    static constexpr int OFFSET = kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES;
+    static_assert(OFFSET % 16 == 0, "table alignment");
     static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<T>) : 0;
     __device__ static __forceinline__ const C2<T>* table(const T* lds) {
         return reinterpret_cast<const C2<T>*>(reinterpret_cast<const char*>(lds) + OFFSET);
@@ -739,7 +641,7 @@ template <typename T, int N, int E> struct TwSplit {
     }
 };
 template <typename T, int N, int E> constexpr int kLdsBytes =
-    kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES + XBuf<T, N, E>::BYTES + TwSplit<T, N, E>::BYTES;
+    kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES + TwSplit<T, N, E>::BYTES;
 
 
 // ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P.
@@ -755,7 +657,7 @@ template <typename T, int N, int E, int OUT, int P, bool XD>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
                                             Stamps* st, void* ocur2 = nullptr, int dma_rounds = 1 << 30,
-                                            const void* xs_next2 = nullptr, double* acc = nullptr) {
+                                            double* acc = nullptr) {
     using S = Sc<T>;
     constexpr bool PAIRSIG = !std::is_same<T, S>::value;
     constexpr int OSZ = (int)sizeof(typename OutT<OUT, S>::type);
@@ -768,7 +670,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
         if constexpr (SPLIT) split = reinterpret_cast<const C2<S>*>(TwSplit<T, N, E>::table(lds));
         C2<S> pb[Q][LR > 0 ? LR : 1];
 #ifndef NW_ABL_NOTWIDDLE
-        if constexpr (!TABLED && I::PAIRED && Q == 2 && NW_TW_PAIR) {
+        if constexpr (!TABLED && I::PAIRED && Q == 2) {
             // the lane's second butterfly is j + 1 (j even, no wrap mod NS): its bases are the
             // first's times the constants w^(2^k) -- uniform loads from the exact table
             twiddle_bases<S, R, N, I::NS * R, SPLIT>(pb[0], I::bfly(t, 0) % I::NS, tw, split);
@@ -781,10 +683,6 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
 #endif
 #ifndef NW_ABL_NOEXCH
         lds_barrier();                         // earlier readers of the image are done
-        if constexpr (P == 1 && XBuf<T, N, E>::ON) {
-            // every wave has read this signal's X: fetch the next one into the buffer
-            if (xs_next) dma_x<T, N, Geometry<N, E>::T>(xs_next, XBuf<T, N, E>::at_lds(lds), t);
-        }
         lds_write<T, N, E, P - 1, 0>(v, lds, t);
         lds_barrier();
         lds_read<T, N, E, P, 0, OSZ>(v, lds, t);
@@ -799,14 +697,8 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
         if constexpr (I::LAST && XD) {
             if (xs_next) {                     // the image is idle once every wave has read it
                 lds_barrier();
-                if constexpr (PAIRSIG) {       // two signals' half spectra, side by side
-                    dma_x<S, N, Geometry<N, E>::T>(reinterpret_cast<const C2<S>*>(xs_next), lds, t, dma_rounds);
-                    if (xs_next2)
-                        dma_x<S, N, Geometry<N, E>::T>(reinterpret_cast<const C2<S>*>(xs_next2),
-                                                       reinterpret_cast<C2<S>*>(lds) + N / 2, t, dma_rounds);
-                } else {
-                    dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t, dma_rounds);
-                }
+                static_assert(!PAIRSIG, "the signal-pair kernel reads X from L2");
+                dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t, dma_rounds);
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -821,11 +713,11 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                     v[q * R + r] = cmul(v[q * R + r], tab[(r - 1) * I::NS]);
                     if (r % 8 == 7) __builtin_amdgcn_sched_barrier(0);   // <= 8 twiddles in flight
                 }
-            } else if constexpr (!(NW_PK && std::is_same<T, float>::value && Q % 2 == 0)) {
+            } else if constexpr (!(std::is_same<T, float>::value && Q % 2 == 0)) {
                 twiddle_apply<T, R>(v + q * R, pb[q]);
             }
 #endif
-            if constexpr (NW_PK && std::is_same<T, float>::value && Q % 2 == 0) {
+            if constexpr (std::is_same<T, float>::value && Q % 2 == 0) {
                 // butterflies q, q+1 as one packed pair: identical DIF networks, per-butterfly
                 // twiddles packed side by side
                 if (q % 2 == 0) {
@@ -895,7 +787,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                     // |y|^2 of fp32 parts is exact in fp64 up to one rounding (no overflow), so
                     // rsqrt replaces hypot + two divisions (k_accumulate) to within a few fp64
                     // ulp; y = 0 gives 0 * inf = NaN like the reference's 0/0 (mneutils.py:68)
-                    const double inv = NW_PHSUM_RSQ ? rsqrt(re * re + im * im) : 1.0 / hypot(re, im);
+                    const double inv = rsqrt(re * re + im * im);
                     // products rounded before the add (no fma into acc): a partial then adds the
                     // same values whichever block boundaries the chunking draws
                     acc[2 * e] += mul_nocontract(re, inv);
@@ -928,7 +820,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                 LastStores<T, N, E, OUT>::all(v, ocur, t);
             }
         } else {
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, xs_next2, acc);
+            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, acc);
         }
     }
 }

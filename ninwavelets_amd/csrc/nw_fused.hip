@@ -37,17 +37,12 @@ __device__ __forceinline__ void load_x(C2<T>* x, const C2<T>* xs, int t) {
     const uint32_t xo = (uint32_t)t * (uint32_t)sizeof(C2<T>);
 #pragma unroll
     for (int r = 0; r < NZ; ++r) {
-#ifdef NW_ABL_NOXLOAD
-        x[r] = {(T)(t + r), (T)r};
-        asm volatile("" : "+v"(x[r].re), "+v"(x[r].im));
-#else
         if (r < E / 2) {
             x[r] = *at(xs, xo, (uint32_t)(r * TT * sizeof(C2<T>)));
         } else {   // X[N - k] = X[(N - r*T) - t]
             x[r] = *at(xs, (uint32_t)((N - r * TT) * sizeof(C2<T>)) - xo);
             x[r].im = -x[r].im;
         }
-#endif
     }
 }
 
@@ -66,66 +61,31 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
     __device__ static __forceinline__ C2<T> apply(C2<T> w, C2<T> x) { return cmul(w, x); }
 };
 
-// Occupancy target: 4 waves per SIMD (<= 128 VGPRs).  The half image is <= 74 KiB
-// (fp32), so two 512-thread blocks share a CU at n = 16384 (more at smaller n) and
-// one block's barriers, memory waits and store bursts overlap another's arithmetic.
-#ifndef NW_DMA_PRUNE
-#define NW_DMA_PRUNE 1   // LDS-DMA of X limited to the pruned pass 0's bins
-#endif
-#ifndef NW_WKEEP32
-#define NW_WKEEP32 16   // measured C4: 0 / 8 / 16 -> 3.537 / 3.486 / 3.456 ms per launch (one box)
-#endif
-#ifndef NW_WKEEP64
-#define NW_WKEEP64 0
-#endif
-#ifndef NW_GROUP
-#define NW_GROUP 8   // measured: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (with NW_TILEG 4)
-#endif
-#ifndef NW_TILEG
-#define NW_TILEG 4   // 8 signal groups x 8 signals x 8 scales per XCD tile
-#endif
-#ifndef NW_TILEF
-#define NW_TILEF 8
-#endif
-constexpr int kGroup = NW_GROUP;   // signals per block
-// XCD tile (scales x signal groups) per element type: fp64 runs one block per CU, so one
-// round of an XCD (32 blocks) is the whole tile
-#ifndef NW_TILEF64
-#define NW_TILEF64 NW_TILEF
-#endif
-#ifndef NW_TILEG64
-#define NW_TILEG64 NW_TILEG
-#endif
-template <typename T> constexpr int kTileFT = sizeof(T) == 8 ? NW_TILEF64 : NW_TILEF;   // scales per XCD tile
-template <typename T> constexpr int kTileGT = sizeof(T) == 8 ? NW_TILEG64 : NW_TILEG;   // signal groups per XCD tile
+// Tuning constants (each measured against its alternatives):
+// E = 32 kernels keep the first kWKeep32 elements of W in registers for the block (a row
+// pruned to NZ <= 16 then reads no W per signal): C4 0 / 8 / 16 -> 3.537 / 3.486 / 3.456 ms
+// per launch; fp64 has no registers to spare (4 and 8 measured +-0 / slower, with spills)
+constexpr int kWKeep32 = 16;
+// signals per block: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (2 and 16 slower or equal)
+constexpr int kGroup = 8;
+// XCD tile: kTileF scales x kTileG signal groups per XCD round (fp64 tiles 16 x 2, 4 x 8,
+// 32 x 1, 2 x 16 measured -2.4 / -0.2 / -4.8 / -3.5 % against 8 x 4)
+constexpr int kTileF = 8, kTileG = 4;
+// Occupancy: 4 waves/SIMD (128 VGPRs) for fp32 -- the half image is <= 74 KiB, so two
+// 512-thread blocks share a CU at n = 16384 (more at smaller n) and one block's barriers,
+// memory waits and store bursts overlap another's arithmetic -- and 2 for fp64 (twice the
+// registers per element); the partial-sum kernels hold fp64 accumulators on top: ITC (2E) at 3 waves/SIMD,
+// power at E = 32 at 2
+constexpr int kWpsF32 = 4, kWpsF64 = 2, kWpsPhSum = 3, kWpsPSum32 = 2;
+template <typename T, int E, int OUT>
+constexpr int kWpsOf = sizeof(T) == 8 ? kWpsF64 : OUT == kOutPhSum ? kWpsPhSum
+                     : (OUT == kOutPSum && E >= 32) ? kWpsPSum32 : kWpsF32;
 
-#ifndef NW_WPS32
-#define NW_WPS32 4
-#endif
-#ifndef NW_WPS16
-#define NW_WPS16 4
-#endif
-// fp64 holds twice the registers per element: 2 waves per SIMD
-#ifndef NW_WPS64
-#define NW_WPS64 2
-#endif
-#define NW_WAVES_PER_SIMD(T, E) (sizeof(T) == 8 ? NW_WPS64 : (E) >= 32 ? NW_WPS32 : NW_WPS16)
-// the ITC partials hold 2E fp64 accumulators (4E VGPRs) on top: one wave per SIMD fewer
-#ifndef NW_WPS_PHSUM
-#define NW_WPS_PHSUM 3
-#endif
-// ... and the power partials at E = 32 hold E fp64 accumulators on top of a 128-VGPR kernel
-#ifndef NW_WPS_PSUM32
-#define NW_WPS_PSUM32 2
-#endif
-#define NW_WPS_OF(T, E, OUT) \
-    (sizeof(T) == 8 ? NW_WPS64 : (OUT) == kOutPhSum ? NW_WPS_PHSUM : ((OUT) == kOutPSum && (E) >= 32) ? NW_WPS_PSUM32 \
-                                                                                                  : NW_WAVES_PER_SIMD(T, E))
 // WSH: the W-row support table wnz was built for the output kernels' E << WSH elements per
 // thread (the partial-sum kernels may run at a smaller E): a row whose elements r >= nz are
 // zero at E << WSH has elements r >= max(1, nz >> WSH) zero here
 template <typename T, int N, int E, int OUT, bool REALW, int WSH = 0>
-__global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
+__global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
                                                             const void* __restrict__ wtab, void* __restrict__ out,
                                                             const C2<T>* __restrict__ tw, int64_t nsig, int group,
                                                             int nsg_pad, const int* __restrict__ wnz) {
@@ -141,7 +101,6 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
     // kTileF scales x kTileG signal groups, so each W row is read by kTileG blocks
     // and each X group by kTileF blocks from L2 (W + X of a tile ~2.5 MiB), and
     // the XCD sweeps all scales of its groups before moving on.
-    constexpr int kTileF = kTileFT<T>, kTileG = kTileGT<T>;
     const int b = blockIdx.x;
     const int xcd = b & 7;
     const int local = b >> 3;
@@ -155,11 +114,11 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
     const int64_t s_end = min(nsig, s_begin + group);
 
     // W[f, k] at the thread's bins (1/n folded in), from the device-built table (L2-shared
-    // by the XCD tile).  E <= NW_WREG_MAX_E: held in registers for the whole block, loaded
+    // by the XCD tile).  E <= kWregMaxE: held in registers for the whole block, loaded
     // before any store is in flight; E = 32: re-read per signal (no VGPRs to spare).
     const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * N;
     const uint32_t wo = (uint32_t)t * (uint32_t)sizeof(WT);
-    constexpr bool WREG = E <= NW_WREG_MAX_E && !(sizeof(T) == 8 && N / E > 512);
+    constexpr bool WREG = E <= kWregMaxE && !(sizeof(T) == 8 && N / E > 512);
     WT w[WREG ? E : 1];
     if constexpr (WREG) {
 #pragma unroll
@@ -168,7 +127,7 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
     // E = 32: the first WKEEP elements of W stay in registers for the block (a row pruned to
     // NZ <= WKEEP reads no W per signal; loads issued after the previous signal's stores
     // wait for all of them in the in-order vmcnt queue)
-    constexpr int WKEEP = (!WREG && REALW) ? (sizeof(T) == 4 ? NW_WKEEP32 : NW_WKEEP64) : 0;
+    constexpr int WKEEP = (!WREG && REALW && sizeof(T) == 4) ? kWKeep32 : 0;
     WT wk[WKEEP > 0 ? WKEEP : 1];
     if constexpr (WKEEP > 0) {
 #pragma unroll
@@ -199,24 +158,22 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
     // XDMA: X[N/2] (the real Nyquist bin, outside the DMA'd half) of the signal being
     // transformed, carried one signal ahead in registers so its load never queues behind
     // a store and is never folded into a private/LDS pointer select
-    constexpr bool XB = XBuf<T, N, E>::ON;
     C2<T> nyq{T(0), T(0)};
-    if constexpr (XD || XB) {
+    if constexpr (XD) {
         nyq = reinterpret_cast<const C2<T>*>(X + s_begin * d.nh)[N / 2];
-        const int nz0 = NW_PRUNE ? max(1, wnz[fi] >> WSH) : E;
-        const int nzv0 = nz0 < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz0;
+        const int nz0 = max(1, wnz[fi] >> WSH);
+        const int nzv0 = nz0 < kPruneMin ? kPruneMin : nz0;
         dma_x<T, N, G::T>(reinterpret_cast<const C2<T>*>(X + s_begin * d.nh),
-                          XD ? (void*)lds : (void*)XBuf<T, N, E>::at_lds(lds), t,
-                          (XD && NW_DMA_PRUNE && nzv0 <= E / 2) ? dma_rounds_for<T>(nzv0) : 1 << 30);
+                          lds, t, nzv0 <= E / 2 ? dma_rounds_for<T>(nzv0) : 1 << 30);
     }
     // W row support (device-built with the table): elements r >= nz of pass 0 multiply an
     // exactly-zero W for every thread of the block (k = t + r*T beyond the row's last
     // nonzero bin), so they are neither read nor multiplied and the DIF stages skip them
-    const int nz = NW_PRUNE ? max(1, wnz[fi] >> WSH) : E;
+    const int nz = max(1, wnz[fi] >> WSH);
     // LDS-DMA only the X bins the pruned pass 0 reads: variant NZ (>= 4) reads bins < NZ*T,
     // i.e. NZ/2 rounds of 2*T bins, when it reads no mirrored bin (NZ <= E/2)
-    const int nzv = nz < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz;
-    const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? dma_rounds_for<T>(nzv) : 1 << 30;
+    const int nzv = nz < kPruneMin ? kPruneMin : nz;
+    const int dma_rounds = nzv <= E / 2 ? dma_rounds_for<T>(nzv) : 1 << 30;
     // power partial sums (kOutPSum): sum over the block's signals of |y|^2 per output point
     // (kOutPhSum: the sums of y / |y|, two fp64 values per point)
     constexpr bool PSUM = OUT == kOutPSum || OUT == kOutPhSum;
@@ -228,18 +185,18 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
     }
     for (int64_t s = s_begin; s < s_end; ++s) {
         const C2<T>* xl = nullptr;
-        if constexpr (XD || XB) {
+        if constexpr (XD) {
             // this wave's DMA landed (only the stores issued after it may be pending),
             // then every wave's: the whole X[0 .. N/2) is in LDS
             // (the partial-sum modes store nothing after the DMA: nothing may stay pending)
             if (s == s_begin || PSUM) wait_vmcnt<0>(); else wait_vmcnt<LastStores<T, N, E, OUT>::COUNT>();
             lds_barrier();
-            xl = XD ? reinterpret_cast<const C2<T>*>(lds) : XBuf<T, N, E>::at_lds(lds);
+            xl = reinterpret_cast<const C2<T>*>(lds);
         }
         C2<T> v[E];
         // pass 0 (Ns = 1): z = W * X at k = t + r*T, r < NZ, radix-E IDFT in registers
         auto pass0 = [&]<int NZ>() {
-            if constexpr (XD || XB) {
+            if constexpr (XD) {
                 // the lane index made opaque HERE: LDS reads are speculatable, and hoisted
                 // above the variant dispatch they would all be live at once and spill
                 int tl = t;
@@ -266,19 +223,17 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
                 v[r] = r < NZ ? WLoad<T, REALW>::apply(w_at(r), x[r]) : C2<T>{T(0), T(0)};
             idft_br<T, E, NZ>(v);
         };
-        if (NW_PRUNE_MIN <= 1 && nz <= 1) pass0.template operator()<1>();
-        else if (NW_PRUNE_MIN <= 2 && nz <= 2) pass0.template operator()<2>();
-        else if (nz <= 4) pass0.template operator()<4>();
+        if (nz <= 4) pass0.template operator()<4>();
         else if (nz <= 8) pass0.template operator()<8>();
         else if (E > 16 && nz <= 16) pass0.template operator()<(E > 16 ? 16 : E)>();
         else pass0.template operator()<E>();
-        if constexpr (XD || XB) {
+        if constexpr (XD) {
             if (s + 1 < s_end) nyq = reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh)[N / 2];
         }
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
         void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
-        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds, nullptr,
+        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds,
                                          PSUM ? acc : nullptr);
     }
     if constexpr (PSUM) {
@@ -313,20 +268,11 @@ __global__ __launch_bounds__(N / E, NW_WPS_OF(T, E, OUT)) void nw_fused_kernel(W
 // (v_pk_add/mul/fma_f32; 8-B image slots; twiddles and the pass-1 table shared).  Pass 0
 // reads both X rows and the block's W registers; the last pass stores each half to its
 // own row (an odd last signal transforms a duplicate whose high half is not stored).
-#ifndef NW_PAIR
-#define NW_PAIR 1
-#endif
-#ifndef NW_PAIR_XDMA
-#define NW_PAIR_XDMA 0   // measured slower: C3 1.257 -> 1.356 ms, n = 1024 / 2048 +4 % (as the single-signal E = 16 XD)
-#endif
-#ifndef NW_WPS_PAIR
-#define NW_WPS_PAIR 4
-#endif
-#ifndef NW_WPS_PAIR_PSUM
-#define NW_WPS_PAIR_PSUM 3   // + E fp64 power accumulators
-#endif
+// X is read from L2 in pass 0 (the next pair's X by LDS-DMA measured slower: C3 1.257 ->
+// 1.356 ms, n = 1024 / 2048 +4 %, as the single-signal E = 16 DMA).  4 waves/SIMD; the power
+// partials' E fp64 accumulators take it to 3.
 template <int N, int E, int OUT>
-__global__ __launch_bounds__(N / E, OUT == kOutPSum ? NW_WPS_PAIR_PSUM : NW_WPS_PAIR) void nw_fused_pair_kernel(WDesc d, const cplx<float>* __restrict__ X,
+__global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_kernel(WDesc d, const cplx<float>* __restrict__ X,
                                                                   const void* __restrict__ wtab, void* __restrict__ out,
                                                                   const C2<float>* __restrict__ tw, int64_t nsig,
                                                                   int group, int nsg_pad, const int* __restrict__ wnz) {
@@ -336,7 +282,6 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? NW_WPS_PAIR_PSUM : NW_WPS_
     f2* lds = reinterpret_cast<f2*>(smem);
     const int t = threadIdx.x;
     // XCD-aware block -> (scale, signal group): as nw_fused_kernel
-    constexpr int kTileF = kTileFT<float>, kTileG = kTileGT<float>;
     const int b = blockIdx.x;
     const int xcd = b & 7;
     const int local = b >> 3;
@@ -356,14 +301,7 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? NW_WPS_PAIR_PSUM : NW_WPS_
     for (int r = 0; r < E; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(float)));
     Tab1<f2, N, E>::fill(lds, tw, t);
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<float>) : sizeof(float));
-    const int nz = NW_PRUNE ? wnz[fi] : E;
-    // PXD: the next pair's two half spectra X[0 .. N/2) are LDS-DMA'd side by side into the
-    // idle image before this pair's stores (as nw_fused_kernel's XD; the pair image of
-    // N + N/16 8-B slots holds both), the real Nyquist bins ride one pair ahead in registers
-    constexpr bool PXD = NW_PAIR_XDMA;
-    const int nzv = nz < NW_PRUNE_MIN ? NW_PRUNE_MIN : nz;
-    const int dma_rounds = (NW_DMA_PRUNE && nzv <= E / 2) ? dma_rounds_for<float>(nzv) : 1 << 30;
-    C2<float> nyqa{0.0f, 0.0f}, nyqb{0.0f, 0.0f};
+    const int nz = wnz[fi];
     auto xrow = [&](int64_t s) { return reinterpret_cast<const C2<float>*>(X + s * d.nh); };
     // power partial sums (kOutPSum): as nw_fused_kernel, both signals of a pair into one sum
     constexpr bool PSUM = OUT == kOutPSum;
@@ -372,77 +310,27 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? NW_WPS_PAIR_PSUM : NW_WPS_
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[e] = 0.0;
     }
-    if constexpr (PXD) {
-        const int64_t s2 = s_begin + 1 < s_end ? s_begin + 1 : s_begin;
-        nyqa = xrow(s_begin)[N / 2];
-        nyqb = xrow(s2)[N / 2];
-        dma_x<float, N, G::T>(xrow(s_begin), lds, t, dma_rounds);
-        dma_x<float, N, G::T>(xrow(s2), reinterpret_cast<C2<float>*>(lds) + N / 2, t, dma_rounds);
-    }
     for (int64_t s = s_begin; s < s_end; s += 2) {
         const bool two = s + 1 < s_end;
         const int64_t s2 = two ? s + 1 : s;
         C2<f2> v[E];
-        if constexpr (PXD) {
-            // this wave's DMAs landed (only the previous pair's stores may be pending), then every wave's
-            if (s == s_begin) wait_vmcnt<0>(); else wait_vmcnt<2 * LastStores<float, N, E, OUT>::COUNT>();
-            lds_barrier();
-        }
         auto pass0 = [&]<int NZ>() {
             C2<float> xa[E], xb[E];
-            if constexpr (PXD) {
-                int tl = t;                    // opaque: the LDS reads must not hoist above the dispatch
-                asm volatile("" : "+v"(tl));
-                const C2<float>* la = reinterpret_cast<const C2<float>*>(lds);
-                const C2<float>* lb = la + N / 2;
-                const C2<float>* ma = la + (N - (E - 1) * G::T - tl);   // X[N - k], r >= E/2: one base,
-                const C2<float>* mb = lb + (N - (E - 1) * G::T - tl);   // positive immediates
-#pragma unroll
-                for (int r = 0; r < NZ; ++r) {
-                    if (r < E / 2) {
-                        xa[r] = la[tl + r * G::T];
-                        xb[r] = lb[tl + r * G::T];
-                    } else {                   // k = N/2 (t = 0, r = E/2) is the Nyquist bin
-                        xa[r] = ma[(E - 1 - r) * G::T];
-                        xb[r] = mb[(E - 1 - r) * G::T];
-                        if (r == E / 2 && t == 0) {
-                            xa[r] = nyqa;
-                            xb[r] = nyqb;
-                        }
-                        xa[r].im = -xa[r].im;
-                        xb[r].im = -xb[r].im;
-                    }
-                }
-            } else {
-                load_x<float, N, E, NZ>(xa, xrow(s), t);
-                load_x<float, N, E, NZ>(xb, xrow(s2), t);
-            }
+            load_x<float, N, E, NZ>(xa, xrow(s), t);
+            load_x<float, N, E, NZ>(xb, xrow(s2), t);
 #pragma unroll
             for (int r = 0; r < E; ++r)
                 v[r] = r < NZ ? C2<f2>{f2{w[r] * xa[r].re, w[r] * xb[r].re}, f2{w[r] * xa[r].im, w[r] * xb[r].im}}
                               : C2<f2>{f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
             idft_br<f2, E, NZ>(v);
         };
-        if (NW_PRUNE_MIN <= 1 && nz <= 1) pass0.template operator()<1>();
-        else if (NW_PRUNE_MIN <= 2 && nz <= 2) pass0.template operator()<2>();
-        else if (nz <= 4) pass0.template operator()<4>();
+        if (nz <= 4) pass0.template operator()<4>();
         else if (nz <= 8) pass0.template operator()<8>();
         else pass0.template operator()<E>();
-        const C2<float>* xn1 = nullptr;
-        const C2<float>* xn2 = nullptr;
-        if constexpr (PXD) {
-            if (s + 2 < s_end) {
-                const int64_t n1 = s + 2, n2 = s + 3 < s_end ? s + 3 : s + 2;
-                xn1 = xrow(n1);
-                xn2 = xrow(n2);
-                nyqa = xn1[N / 2];
-                nyqb = xn2[N / 2];
-            }
-        }
         void* o1 = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;
         void* o2 = two ? (void*)((char*)out + (s2 * d.nfreq + fi) * (int64_t)N * out_esz) : nullptr;
-        passes_from<f2, N, E, OUT, 1, PXD>(v, lds, t, tw, nullptr, reinterpret_cast<const C2<f2>*>(xn1), o1,
-                                           nullptr, o2, dma_rounds, xn2, PSUM ? acc : nullptr);
+        passes_from<f2, N, E, OUT, 1, false>(v, lds, t, tw, nullptr, nullptr, o1, nullptr, o2, 1 << 30,
+                                             PSUM ? acc : nullptr);
     }
     if constexpr (PSUM) {
         using IL = PassInfo<N, E, G::npass() - 1, (int)sizeof(float), true>;
@@ -459,7 +347,7 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? NW_WPS_PAIR_PSUM : NW_WPS_
 // pass machinery on v[r] = x[t + r*T] (imaginary parts zero), X[k] = conj(y[k]) for k <= n/2
 // (scipy/rocFFT's unnormalised forward transform, base.py:399).
 template <typename T, int N, int E>
-__global__ __launch_bounds__(N / E, NW_WAVES_PER_SIMD(T, E)) void fwd_r2c_kernel(const T* __restrict__ x,
+__global__ __launch_bounds__(N / E, sizeof(T) == 8 ? kWpsF64 : kWpsF32) void fwd_r2c_kernel(const T* __restrict__ x,
                                                                               C2<T>* __restrict__ X,
                                                                               const C2<T>* __restrict__ tw,
                                                                               int64_t nh) {
@@ -596,7 +484,7 @@ size_t wtab_row_bytes(int64_t n, int nfreq, size_t esz, bool realw) {
 }
 
 template <typename T, int E, bool REALW>
-constexpr bool kPairMode = NW_PAIR && std::is_same<T, float>::value && E <= 16 && REALW;
+constexpr bool kPairMode = std::is_same<T, float>::value && E <= 16 && REALW;
 
 template <typename T, int N, int E, bool REALW>
 hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
@@ -606,7 +494,6 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
-    constexpr int kTileF = kTileFT<T>, kTileG = kTileGT<T>;
     const int64_t nsg = (nsig + kGroup - 1) / kGroup;
     const int64_t nsg_pad = (nsg + 8 * kTileG - 1) / (8 * kTileG) * (8 * kTileG);
     const int64_t nfr = (d.nfreq + kTileF - 1) / kTileF;
@@ -637,13 +524,9 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     return hipGetLastError();
 }
 
-#ifndef NW_PAIR_PSUM
-#define NW_PAIR_PSUM 1
-#endif
 template <typename T, int N, int E, int OUT, int WSH>
 hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* partials, int64_t nsig, hipStream_t s) {
     constexpr int threads = N / E;
-    constexpr int kTileF = kTileFT<T>, kTileG = kTileGT<T>;
     const int lds = kLdsBytes<T, N, E>;
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
@@ -658,7 +541,7 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
     if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
     const int* wnz = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
                                                   wtab_row_bytes(N, d.nfreq, sizeof(T), true));
-    if constexpr (OUT == kOutPSum && NW_PAIR_PSUM && kPairMode<T, E, true>) {
+    if constexpr (OUT == kOutPSum && kPairMode<T, E, true>) {
         // power partials on the signal-pair kernel: the same values as its power output
         const int lp = kLdsBytes<f2, N, E>;
         e = hipFuncSetAttribute((const void*)nw_fused_pair_kernel<N, E, kOutPSum>,
@@ -714,10 +597,6 @@ hipError_t prepare_n() {
 
 hipError_t fused_twiddles(int64_t n, int dtype, void** out) { return twiddles_for(n, dtype, out); }
 
-#ifndef NW_E16384
-#define NW_E16384 32   // elements per thread at n = 16384 fp32 (512 threads)
-#endif
-
 // power-of-two n: 2^10..2^14 in fp32 and fp64 (fp64 at 8192 / 16384: E = 32 with 256 VGPRs,
 // W re-read per signal)
 bool fused_supported(int64_t n, int dtype) {
@@ -725,26 +604,14 @@ bool fused_supported(int64_t n, int dtype) {
     return (dtype == NW_F32 || dtype == NW_F64) && n <= 16384;
 }
 
-#ifndef NW_E4096
-#define NW_E4096 16   // E = 32 measured slower here (0.350 -> 0.404 ms power)
-#endif
-#ifndef NW_E8192
-#define NW_E8192 32   // measured: n = 8192 power 0.887 -> 0.768 ms, cwt 1.034 -> 0.926 ms vs E = 16
-#endif
-// fp64 at n >= 8192: E = 32 (3 passes, 256 VGPRs, 2 waves/SIMD, 2 blocks per CU at 8192)
-// instead of E = 16 (4 passes: 16-16-16-2/4, one 512-thread block per CU at 8192).
-// Measured (256 signals x 256 scales): 8192 cwt 2.907 -> 2.573 ms, power 2.397 -> 1.991;
-// 16384 (128 signals) cwt 3.447 -> 3.124, power 2.615 -> 2.312.
-#ifndef NW_E8192_64
-#define NW_E8192_64 32
-#endif
-#ifndef NW_E16384_64
-#define NW_E16384_64 32
-#endif
+// Elements per thread E of each fused size (threads = n / E).  Measured: fp32 n = 4096 at
+// E = 32 slower (0.350 -> 0.404 ms power); n = 8192 at E = 32 vs 16: power 0.887 -> 0.768 ms,
+// cwt 1.034 -> 0.926; fp64 at n >= 8192: E = 32 (3 passes, 256 VGPRs, 2 waves/SIMD) vs E = 16
+// (4 passes): 8192 cwt 2.907 -> 2.573 ms, power 2.397 -> 1.991; 16384 cwt 3.447 -> 3.124,
+// power 2.615 -> 2.312 (256 x 256 rows; 128 x 256 at 16384).
 #define NW_FUSED_TABLE(X)                                                               \
-    X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, NW_E4096) X(float, 8192, NW_E8192) \
-    X(float, 16384, NW_E16384) X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) \
-    X(double, 8192, NW_E8192_64) X(double, 16384, NW_E16384_64)
+    X(float, 1024, 16) X(float, 2048, 16) X(float, 4096, 16) X(float, 8192, 32) X(float, 16384, 32) \
+    X(double, 1024, 16) X(double, 2048, 16) X(double, 4096, 16) X(double, 8192, 32) X(double, 16384, 32)
 
 hipError_t fused_prepare(int64_t n, int dtype) {
 #define NW_PREP(TY, NN, EE) \
@@ -786,12 +653,6 @@ hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
 }
 
 // epoch power / phase partials: analytic rows; fp32 power to E = 32, fp32 phases and fp64 at E = 16
-#ifndef NW_FUSED_PSUM
-#define NW_FUSED_PSUM 1
-#endif
-#ifndef NW_PSUM_MAXE
-#define NW_PSUM_MAXE 32   // power partials up to E = 32 (N = 8192, 16384)
-#endif
 // Elements per thread of the partial-sum kernels (EO: the output kernels'): fp32 power keeps
 // EO (E = 32 at n = 8192 / 16384: E fp64 accumulators at 2 waves/SIMD); fp32 phases (2E fp64
 // accumulators) and fp64 (the drop-in's default dtype, 2 waves/SIMD already at 256 VGPRs)
@@ -804,9 +665,9 @@ template <int EO, int E> constexpr int kPsShift = EO == E ? 0 : EO == 2 * E ? 1 
 // (n = 16384, E = 16) a wave has 128 VGPRs, and neither fp64 power (228 B of scratch) nor
 // phases (fp32: 84 B) fit there -- n = 16384 keeps the chunk path for those
 template <typename T, int N, int EO>
-constexpr bool kPSumOK = NW_FUSED_PSUM && !(sizeof(T) == 8 && N / kPsE<T, EO, false> > 512);
+constexpr bool kPSumOK = !(sizeof(T) == 8 && N / kPsE<T, EO, false> > 512);
 template <typename T, int N, int EO>
-constexpr bool kPhSumOK = NW_FUSED_PSUM && N / kPsE<T, EO, true> <= 512;
+constexpr bool kPhSumOK = N / kPsE<T, EO, true> <= 512;
 
 bool fused_psum_supported(int64_t n, int dtype, int kind, bool phase) {
     if (kind == NW_TABLE) return false;
@@ -822,7 +683,7 @@ int64_t fused_psum_groups(int64_t nsig) { return (nsig + kGroup - 1) / kGroup; }
 int fused_psum_kernel_id(int64_t n, int dtype, bool phase) {
 #define NW_PK_ID(TY, NN, EE) \
     if (n == NN && dtype == (sizeof(TY) == 4 ? NW_F32 : NW_F64)) \
-        return (!phase && NW_PAIR_PSUM && kPairMode<TY, EE, true>) ? NW_K_FUSED_PAIR : NW_K_FUSED;
+        return (!phase && kPairMode<TY, EE, true>) ? NW_K_FUSED_PAIR : NW_K_FUSED;
     NW_FUSED_TABLE(NW_PK_ID)
 #undef NW_PK_ID
     return NW_K_NONE;

@@ -49,29 +49,21 @@ namespace {
 constexpr int kRowGroup = 4;      // rows (k1) per rows_kernel workgroup (1 when a launch holds few scales)
 constexpr int kRowTileF = 8;      // scales per XCD tile
 constexpr int kRowTileG = 8;      // row groups per XCD tile
-#ifndef NW_COL_THREADS
-#define NW_COL_THREADS 1024   // C = 32 columns at N1 = 1024: 256-B runs; measured C5 cols 1.039 -> 0.978 ms vs 512
-#endif
-#ifndef NW_COL_THREADS64
-#define NW_COL_THREADS64 1024
-#endif
+// cols_kernel workgroups of 1024 threads: C = 32 columns at N1 = 1024, 256-B runs (C5 cols
+// 1.039 -> 0.978 ms per launch against 512 threads)
 // cols_kernel workgroup size (C * N1 / E)
-template <typename T> constexpr int kColThreads = sizeof(T) == 4 ? NW_COL_THREADS : NW_COL_THREADS64;
+template <typename T> constexpr int kColThreads = 1024;
 constexpr size_t kBBudget = size_t(2) << 30;   // bytes of B per launch pair (scales chunked to fit)
 
 // N2 (on-chip rows) and its elements per thread E: the nw_fused sizes (fp64: E = 16, N2 <= 8192)
-#ifndef NW_ROWE64
-#define NW_ROWE64 32
-#endif
-template <typename T, int N2> constexpr int kRowE = N2 >= 8192 ? (sizeof(T) == 4 ? 32 : NW_ROWE64) : 16;
+template <typename T, int N2> constexpr int kRowE = N2 >= 8192 ? 32 : 16;
 // complex table rows (wavelet_bin loads) spill at fp64 E = 32: E = 16 there
 template <typename T, int N2> constexpr int kRowETab = sizeof(T) == 8 ? 16 : kRowE<T, N2>;
 // elements per thread in cols_kernel: 32 complex fp32 or 16 complex fp64 (64 VGPRs either way)
 template <typename T> constexpr int kColE = sizeof(T) == 4 ? 32 : 16;
-#ifndef NW_MAXN2_64
-#define NW_MAXN2_64 16384   // measured at C5 fp64: 8192 (N1 = 2048, 8-column blocks, 128-B runs) 150.0 ms/step, 16384 (N1 = 1024, 16 columns, 256-B runs) 129.9
-#endif
-template <typename T> constexpr int kMaxN2 = sizeof(T) == 4 ? 16384 : NW_MAXN2_64;
+// rows of at most 16384 on chip, fp64 too (N2 = 8192 with N1 = 2048, 8-column blocks and
+// 128-B runs: C5 fp64 150.0 ms/step; 16384, 16 columns, 256-B runs: 129.9)
+template <typename T> constexpr int kMaxN2 = 16384;
 
 // ---- X (R2C half spectrum) -> Xt[k1][k2], mirrored + masked (spectrum_bin)
 template <typename T>
@@ -158,25 +150,12 @@ template <int KIND> struct RowW<float, KIND> {
 
 // fp64: psi_f64 (the reference's expression order: pow / exp on nu = j * delta, nu / f)
 // times 1/n, exactly as wavelet_bin<double>, with the per-scale loads hoisted
-#ifndef NW_MORSE_IPOW
-#define NW_MORSE_IPOW 0   // measured: C5 fp64 rows 59.7 -> 93.8 ms/step (the N2 = 16384 Morse rows kernel
-                          // spills 76 B with it), so off
-#endif
-
-__device__ __forceinline__ double ipow(double x, int e) {   // x^e, e >= 0 (uniform e)
-    double acc = 1.0;
-    while (e) {
-        if (e & 1) acc *= x;
-        x *= x;
-        e >>= 1;
-    }
-    return acc;
-}
+// (x^b and x^r by repeated squaring instead of log / exp for small integer 2b and r measured
+// slower: its 76 B of scratch made the C5 fp64 row pass 59.7 -> 93.8 ms per step; x^3 alone,
+// round 3: 44 B of scratch, rows 0.93 -> 0.98 ms per launch)
 template <int KIND> struct RowW<double, KIND> {
     double delta, f, peak, b, r, bor, sigma, cpi, kappa, scale;
     int off, lenv;
-    int bi, ri;       // Morse with 2b and r small integers (the default 17.5, 3): x^b and x^r
-    bool bhalf, ipw;  // by multiplications (+ one sqrt) and ONE exp -- no log, no second exp
     __device__ __forceinline__ void init(const WDesc& d, int fi) {
         delta = d.delta;
         f = d.freq ? d.freq[fi] : 1.0;
@@ -190,11 +169,6 @@ template <int KIND> struct RowW<double, KIND> {
         scale = d.scale;
         off = (int)d.off;
         lenv = d.len_valid < 0x7fffffff ? (int)d.len_valid : 0x7fffffff;
-        ipw = NW_MORSE_IPOW && b >= 0.0 && b <= 64.0 && 2.0 * b == rint(2.0 * b) && r >= 1.0 && r <= 8.0 &&
-              r == rint(r);
-        bi = ipw ? (int)floor(b) : 0;
-        bhalf = ipw && b - floor(b) == 0.5;
-        ri = ipw ? (int)r : 0;
     }
     __device__ __forceinline__ double operator()(int j) const {
         if ((unsigned)j >= (unsigned)lenv) return 0.0;
@@ -206,18 +180,8 @@ template <int KIND> struct RowW<double, KIND> {
             // support; psi(0) = 0 as np.heaviside(0, 0))
             const double x = nu / f;
             if (!(x > 0.0)) return 0.0;
-            if (ipw) {
-                // 2 x^b e^{(b/r)(1 - x^r)}: a few ulp from pow (<< the 1e-12 tolerance); where
-                // x^b would overflow the exponential is already exactly 0
-                const double e = exp(bor * (1.0 - ipow(x, ri)));
-                if (e == 0.0) return 0.0;
-                double xb = ipow(x, bi);
-                if (bhalf) xb *= sqrt(x);
-                psi = 2.0 * xb * e;
-            } else {
-                const double lx = log(x);
-                psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
-            }
+            const double lx = log(x);
+            psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
         } else if constexpr (KIND == NW_MORLET) {
             const double x = nu / f * peak;
             const double a = sigma - x;
@@ -230,19 +194,14 @@ template <int KIND> struct RowW<double, KIND> {
 };
 
 // ---- pass 1: rows
-#ifndef NW_ROWS_XDMA
-#define NW_ROWS_XDMA 1   // fp32 E = 32 rows: pruned Xt rows by LDS-DMA ahead of the stores
-#endif
-// (analytic kinds only: table rows' wavelet_bin loads would exceed 128 VGPRs, as in nw_fused)
-#ifndef NW_ROWS_XDMA64
-#define NW_ROWS_XDMA64 0
-#endif
+// fp32 E = 32 rows: pruned Xt rows by LDS-DMA ahead of the stores (C5 50.6 -> 48.5 ms per step);
+// analytic kinds only (table rows' wavelet_bin loads would exceed 128 VGPRs, as in nw_fused);
+// fp64 rows with the same DMA measured no faster (0.94 -> 0.98 ms per launch)
 template <typename T, int E, int KIND>
-constexpr bool kRowsXD = NW_ROWS_XDMA && (sizeof(T) == 4 || NW_ROWS_XDMA64) && E >= 32 && KIND != NW_TABLE;
-#define NW_LARGE_WPS 4
-#define NW_LARGE_WPS64 2   // fp64: twice the registers per element (as nw_fused)
+constexpr bool kRowsXD = sizeof(T) == 4 && E >= 32 && KIND != NW_TABLE;
+// 4 waves/SIMD; fp64: 2 (twice the registers per element, as nw_fused)
 template <typename T, int N2, int E, int KIND>
-__global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? NW_LARGE_WPS64 : NW_LARGE_WPS) void rows_kernel(
+__global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
     WDesc d, int f0, int nf, int n1, int rgs, const C2<T>* __restrict__ Xt, C2<T>* __restrict__ B,
     const int* __restrict__ kmax, const C2<T>* __restrict__ tw) {
     using G = Geometry<N2, E>;
@@ -705,13 +664,8 @@ hipError_t cols_t(const WDesc& d, int out_kind, int f0, int nf, const void* supp
         NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(32, 16384)
         NW_COLS(64, 16384) NW_COLS(128, 16384) NW_COLS(256, 16384) NW_COLS(512, 16384) NW_COLS(1024, 16384)
     } else {
-#if NW_MAXN2_64 == 8192
-        NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(64, 8192)
-        NW_COLS(128, 8192) NW_COLS(256, 8192) NW_COLS(512, 8192) NW_COLS(1024, 8192) NW_COLS(2048, 8192)
-#else
         NW_COLS(32, 1024) NW_COLS(32, 2048) NW_COLS(32, 4096) NW_COLS(32, 8192) NW_COLS(32, 16384)
         NW_COLS(64, 16384) NW_COLS(128, 16384) NW_COLS(256, 16384) NW_COLS(512, 16384) NW_COLS(1024, 16384)
-#endif
     }
     return hipErrorNotSupported;
 #undef NW_COLS
