@@ -66,11 +66,21 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
 // pruned to NZ <= 16 then reads no W per signal): C4 0 / 8 / 16 -> 3.537 / 3.486 / 3.456 ms
 // per launch; fp64 has no registers to spare (4 and 8 measured +-0 / slower, with spills)
 constexpr int kWKeep32 = 16;
-// signals per block: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (2 and 16 slower or equal)
+// signals per block: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (2 and 16 slower or equal).
+// fp64 (one block per CU) takes 4: an XCD round of 8 scales x 4 groups then reads W (8 x 128
+// KiB) + X (16 x 128 KiB) = 3 MiB, inside the XCD's 4 MiB L2 (8 signals: 5 MiB, re-read from
+// the Infinity Cache); the C4 shape in fp64 10.04 -> 9.66 ms per launch (2 / 3 signals:
+// 9.55 / 9.40, 16: 9.71; two boxes, tools/ab.sh)
 constexpr int kGroup = 8;
+#ifndef NW_GROUP64
+#define NW_GROUP64 4
+#endif
+constexpr int kGroup64 = NW_GROUP64;
 // XCD tile: kTileF scales x kTileG signal groups per XCD round (fp64 tiles 16 x 2, 4 x 8,
 // 32 x 1, 2 x 16 measured -2.4 / -0.2 / -4.8 / -3.5 % against 8 x 4)
 constexpr int kTileF = 8, kTileG = 4;
+template <typename T> constexpr int kTileFT = kTileF;
+template <typename T> constexpr int kTileGT = kTileG;
 // Occupancy: 4 waves/SIMD (128 VGPRs) for fp32 -- the half image is <= 74 KiB, so two
 // 512-thread blocks share a CU at n = 16384 (more at smaller n) and one block's barriers,
 // memory waits and store bursts overlap another's arithmetic -- and 2 for fp64 (twice the
@@ -104,11 +114,12 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     const int b = blockIdx.x;
     const int xcd = b & 7;
     const int local = b >> 3;
-    const int pos = local % (kTileF * kTileG);
-    const int round = local / (kTileF * kTileG);
-    const int nfr = (d.nfreq + kTileF - 1) / kTileF;
-    const int fi = (round % nfr) * kTileF + pos % kTileF;
-    const int sg = ((round / nfr) * kTileG + pos / kTileF) * 8 + xcd;
+    constexpr int TF = kTileFT<T>, TG = kTileGT<T>;
+    const int pos = local % (TF * TG);
+    const int round = local / (TF * TG);
+    const int nfr = (d.nfreq + TF - 1) / TF;
+    const int fi = (round % nfr) * TF + pos % TF;
+    const int sg = ((round / nfr) * TG + pos / TF) * 8 + xcd;
     if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
     const int64_t s_begin = (int64_t)sg * group;
     const int64_t s_end = min(nsig, s_begin + group);
@@ -494,10 +505,12 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
-    const int64_t nsg = (nsig + kGroup - 1) / kGroup;
-    const int64_t nsg_pad = (nsg + 8 * kTileG - 1) / (8 * kTileG) * (8 * kTileG);
-    const int64_t nfr = (d.nfreq + kTileF - 1) / kTileF;
-    const int64_t blocks = nsg_pad * nfr * kTileF;
+    const int grp = sizeof(T) == 8 ? kGroup64 : kGroup;
+    const int64_t nsg = (nsig + grp - 1) / grp;
+    constexpr int TF = kTileFT<T>, TG = kTileGT<T>;
+    const int64_t nsg_pad = (nsg + 8 * TG - 1) / (8 * TG) * (8 * TG);
+    const int64_t nfr = (d.nfreq + TF - 1) / TF;
+    const int64_t blocks = nsg_pad * nfr * TF;
     if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
     const cplx<T>* Xc = reinterpret_cast<const cplx<T>*>(X);
     const C2<T>* twc_ = reinterpret_cast<const C2<T>*>(tw);
@@ -516,11 +529,11 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
         return hipGetLastError();
     }
     if (out_kind == NW_OUT_CWT)
-        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad, wnz);
+        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz);
     else if (out_kind == NW_OUT_POWER)
-        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad, wnz);
+        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz);
     else
-        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, kGroup, (int)nsg_pad, wnz);
+        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz);
     return hipGetLastError();
 }
 
@@ -535,9 +548,10 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     const int64_t nsg = (nsig + kGroup - 1) / kGroup;
-    const int64_t nsg_pad = (nsg + 8 * kTileG - 1) / (8 * kTileG) * (8 * kTileG);
-    const int64_t nfr = (d.nfreq + kTileF - 1) / kTileF;
-    const int64_t blocks = nsg_pad * nfr * kTileF;
+    constexpr int TF = kTileFT<T>, TG = kTileGT<T>;
+    const int64_t nsg_pad = (nsg + 8 * TG - 1) / (8 * TG) * (8 * TG);
+    const int64_t nfr = (d.nfreq + TF - 1) / TF;
+    const int64_t blocks = nsg_pad * nfr * TF;
     if (blocks > 0x7fffffff || nsg_pad > 0x7fffffff) return hipErrorInvalidConfiguration;
     const int* wnz = reinterpret_cast<const int*>(reinterpret_cast<const char*>(wtab) +
                                                   wtab_row_bytes(N, d.nfreq, sizeof(T), true));
