@@ -594,8 +594,16 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     // over each block of 8 signals in fp64, the accumulator adds the ceil(c / 8) fp64 partials
     // (the same fp64 additions of the same fp32-derived values, regrouped; with the dedup view
     // the partials of the distinct rows are expanded like any output row)
-    const bool psum = fused && !p->large && !p->chirp &&
-                      nw::fused_psum_supported(p->n, p->dtype, p->desc.kind, phase);
+    // The chirp-z form (lengths 2n - 1 <= M_max, every row on chip) read-modify-writes its
+    // block partial rows instead (no accumulator registers; any kind, fp32 and fp64); its
+    // tentative lengths (rows may leave the chip) and the repeated-row view keep the chunk path
+    bool chirp_psum = fused && p->chirp && !p->chirp_tentative && !p->dedup;
+    if (chirp_psum) {
+        NW_TRY(chirp_table(p));   // the rows' M classes decide (chirp_psum_ok)
+        chirp_psum = p->chirp && p->chirp_over.empty() && nw::chirp_psum_ok(p->dtype, phase, p->chirp_counts);
+    }
+    const bool psum = (fused && !p->large && !p->chirp &&
+                       nw::fused_psum_supported(p->n, p->dtype, p->desc.kind, phase)) || chirp_psum;
     const int sig_kind = psum ? (phase ? OUT_PHSUM : OUT_PSUM) : (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
     // partials: plain fp64 sums (phase partials as 2 fn reals)
     const int src_kind = psum ? nw::ACC_POWER_REAL

@@ -97,10 +97,11 @@ template <typename T> struct WRow<T, false> {
 // waves per SIMD without scratch (tools/regs.py): fp32 M <= 4096 fit 168 VGPRs (3 waves;
 // 4 spilled 44 B at M = 1024), M >= 8192 and fp64 need up to 256 (2 waves; fp32 M = 16384
 // at E = 32 still spills ~230 B there)
-template <typename T, int M, int E>
-constexpr int kChirpWps = E <= 8 ? 4 : (sizeof(T) == 4 && M <= 4096 && E <= 16) ? 3 : 2;
+// (the phase-sum form holds the chirp and the reciprocal on top: 2 waves/SIMD, no scratch)
+template <typename T, int M, int E, int OUT>
+constexpr int kChirpWps = OUT == kOutPhSum ? 2 : E <= 8 ? 4 : (sizeof(T) == 4 && M <= 4096 && E <= 16) ? 3 : 2;
 template <typename T, int M, int E, int OUT, bool REALW>
-__global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
+__global__ __launch_bounds__(M / E, (kChirpWps<T, M, E, OUT>)) void nw_chirp_kernel(
     WDesc d, const cplx<T>* __restrict__ X, const void* __restrict__ wtab, void* __restrict__ out,
     const C2<T>* __restrict__ tw, const C2<T>* __restrict__ bh, const C2<T>* __restrict__ ct, int64_t nsig,
     int nsg_pad, const int* __restrict__ rowmap, int nrows, const int* __restrict__ ksup) {
@@ -180,19 +181,52 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E>)) void nw_chirp_kernel(
         passes_regs<T, M, E, 1>(v, lds, t, tw);
         // y[n] = c(n) y'[n] for n < N (|y|, |y|^2: |c(n)| = 1, the chirp is skipped)
         O* orow = reinterpret_cast<O*>(out) + (s * d.nfreq + fi) * (int64_t)n;
+        // epoch partial sums (kOutPSum / kOutPhSum): the block's fp64 row (group sg, scale fi)
+        // of the (groups, F, n) partial buffer, read-modify-written by the lane that owns each
+        // point (the same lane for every signal), in signal order -- no accumulator registers
+        constexpr bool PS = OUT == kOutPSum || OUT == kOutPhSum;
+        constexpr int NACC = OUT == kOutPhSum ? 2 : 1;
+        double* prow = reinterpret_cast<double*>(out) + ((int64_t)sg * d.nfreq + fi) * (int64_t)n * NACC;
+        const bool first = s == s_begin;
 #pragma unroll
         for (int q = 0; q < IL::Q; ++q) {
             // outputs n_j = n0 + j*NS in natural j order (register i = bitrev(j)); |y| and
             // |y|^2 skip the final chirp (|c(n) y'| = |y'|: n = 1201 power 1.397 -> 1.313 ms)
             const uint32_t n0 = (uint32_t)(t + q * TT);
-            constexpr bool EPI = OUT == NW_OUT_CWT;
+            constexpr bool EPI = OUT == NW_OUT_CWT || OUT == kOutPhSum;
 #pragma unroll
             for (int j = 0; j < IL::R; ++j) {
                 const int i = bitrev<IL::R>(j);
                 const int idx = (int)n0 + j * IL::NS;
                 C2<T> y = v[q * IL::R + i];
                 if constexpr (EPI) y = cmul(y, chirp<T>(idx, n2, inv_n2, ct));
-                if (idx < n) orow[idx] = out_value<OUT, T>(y);
+                if constexpr (OUT == kOutPSum) {
+                    // the power output's own value (out_value), added in fp64 like k_accumulate
+                    const double pv = (double)out_value<NW_OUT_POWER, T>(y);
+                    if (idx < n) prow[idx] = first ? pv : prow[idx] + pv;
+                } else if constexpr (OUT == kOutPhSum) {
+                    // y / |y| (fp64 y: 1 / hypot, which does not underflow; fp32: rsqrt of the
+                    // exact fp64 |y|^2), 0 / 0 -> NaN like the reference (mneutils.py:68)
+                    const double re = (double)y.re, im = (double)y.im;
+                    const double inv = sizeof(T) == 8 ? 1.0 / hypot(re, im) : rsqrt(re * re + im * im);
+                    const double pr = mul_nocontract(re, inv), pi = mul_nocontract(im, inv);
+                    if (idx < n) {
+                        double2* q2 = reinterpret_cast<double2*>(prow) + idx;
+                        if (first) {
+                            *q2 = double2{pr, pi};
+                        } else {
+                            const double2 o = *q2;
+                            *q2 = double2{o.x + pr, o.y + pi};
+                        }
+                    }
+                } else {
+                    if (idx < n) orow[idx] = out_value<OUT, T>(y);
+                }
+                // partial sums: at most 4 read-modify-writes in flight (their loaded values
+                // would otherwise all be live at once and spill)
+                if constexpr (PS) {
+                    if (j % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+                }
             }
         }
     }
@@ -348,7 +382,15 @@ hipError_t launch_m_e(const WDesc& d, int out_kind, const void* X, const void* w
     };
     if (out_kind == NW_OUT_CWT) go(nw_chirp_kernel<T, M, E, NW_OUT_CWT, REALW>);
     else if (out_kind == NW_OUT_POWER) go(nw_chirp_kernel<T, M, E, NW_OUT_POWER, REALW>);
-    else go(nw_chirp_kernel<T, M, E, NW_OUT_ABS, REALW>);
+    else if (out_kind == kOutPSum || out_kind == kOutPhSum) {
+        // partial sums at E = 16 only (chirp_psum_ok: the classes whose kernels do not spill)
+        if constexpr (E == 16) {
+            if (out_kind == kOutPSum) go(nw_chirp_kernel<T, M, E, kOutPSum, REALW>);
+            else go(nw_chirp_kernel<T, M, E, kOutPhSum, REALW>);
+        } else {
+            e = hipErrorNotSupported;
+        }
+    } else go(nw_chirp_kernel<T, M, E, NW_OUT_ABS, REALW>);
     return e;
 }
 
@@ -360,7 +402,7 @@ hipError_t launch_m(const WDesc& d, int out_kind, const void* X, const void* wta
                     const int* rowmap, int nrows, const int* ksup, hipStream_t s) {
     constexpr int EP = (sizeof(T) == 4 && M == 8192) ? 32 : E;
     if constexpr (EP != E) {
-        if (out_kind != NW_OUT_CWT)
+        if (out_kind == NW_OUT_POWER || out_kind == NW_OUT_ABS)
             return launch_m_e<T, M, EP, REALW>(d, out_kind, X, wtab, out, nsig, rowmap, nrows, ksup, s);
     }
     return launch_m_e<T, M, E, REALW>(d, out_kind, X, wtab, out, nsig, rowmap, nrows, ksup, s);
@@ -447,6 +489,18 @@ hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t
     e = hipMemcpyAsync(rowmap, map.data(), map.size() * sizeof(int), hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipStreamSynchronize(s);
     return e;
+}
+
+// Epoch partial sums on the chirp-z form: every M class of the wavelet needs a partial-sum
+// kernel without scratch (tools/regs.py): fp32 M <= 8192 (E = 16), fp64 power every M, fp64
+// phases M <= 2048 (44-60 B of scratch above)
+bool chirp_psum_ok(int dtype, bool phase, const int64_t* counts) {
+    for (int c = 0; c < kChirpClasses; ++c) {
+        if (counts[c] == 0) continue;
+        const int64_t m = 1024ll << c;
+        if (dtype == NW_F32 ? m > 8192 : (phase && m > 2048)) return false;
+    }
+    return true;
 }
 
 hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,

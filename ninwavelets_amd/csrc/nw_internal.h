@@ -202,6 +202,7 @@ hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t
                               std::vector<int>* overflow);
 hipError_t launch_chirp(const WDesc& d, int dtype, int out_kind, const void* X, const void* wtab, void* out,
                         int64_t nsig, const int64_t* counts, hipStream_t s);
+bool chirp_psum_ok(int dtype, bool phase, const int64_t* counts);
 
 // two-pass engine for long signals (nw_large.hip): power-of-two 2^15 <= n <= 2^24, fp32 or
 // fp64.  scratch = Xt (n complex) + B (large_fchunk scales x n complex); support = kmax[nfreq]

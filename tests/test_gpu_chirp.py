@@ -186,3 +186,40 @@ def test_chirp_hybrid_reductions_and_repeated_rows(dtype, n):
     got = p2.execute(x, out_kind='cwt')
     assert p2.stats()['unique_rows'] == 2 and p2.stats()['engine'] == 'fused'
     assert within(got, oracle('morse', x, rep, 'cwt'), dtype, 'cwt')
+
+
+@pytest.mark.parametrize('dtype,n', [('float64', 1201), ('float64', 701), ('float32', 1201), ('float32', 4097)])
+def test_chirp_fused_epoch_partials(dtype, n):
+    """Epoch reductions on the chirp-z form (MNE lengths, mneutils.py:42-71): the kernel
+    read-modify-writes one fp64 partial row per block of 8 signals (signal order) instead of
+    writing every signal's row.  power_sum equals the sum of the same plan's per-signal power
+    output (fp64: the same values, regrouped fp64 additions: 1e-13; fp32: 1e-6); chunk-size
+    independent;
+    ITC against the same plan's materialised cwt; both against the oracle.  fp64 phases run
+    fused only where every row's transform is M <= 2048 (N = 701, 1201 at the C3 scale list)."""
+    S, freqs = 19, np.arange(1, 257, dtype=np.float64)
+    x = synth(S, n, seed=n + 17).astype(dtype)
+    g = L.trans_grid(n / 1000., 1000., False)
+    plan = nw.Plan(n, 256, dtype, max_batch=8)
+    plan.set_wavelet('morse', [17.5, 3.], freqs, g)
+    pw = plan.execute(x, out_kind='power').astype(np.float64)
+    assert L.KERNEL_NAMES[plan.stats()['kernel']] == 'nw_chirp_kernel'
+    ps = plan.execute(x, out_kind='power_sum')
+    # fp32: the partial-sum instantiation (E = 16, 2 waves/SIMD) is scheduled apart from the
+    # power output's (3 waves/SIMD; E = 32 at M = 8192), which moves fp32 values of y by a few
+    # ulp: held to the fp32 contract
+    np.testing.assert_allclose(ps, pw.sum(axis=0), rtol=1e-13 if dtype == 'float64' else 1e-5)
+    other = nw.Plan(n, 256, dtype, max_batch=3)
+    other.set_wavelet('morse', [17.5, 3.], freqs, g)
+    np.testing.assert_allclose(other.execute(x, out_kind='power_sum'), ps, rtol=1e-13)
+    c = plan.execute(x, out_kind='cwt').astype(np.complex128)
+    itc = plan.execute(x, out_kind='itc')
+    ref_itc = np.abs(np.mean(c / np.abs(c), axis=0))
+    assert np.max(np.abs(itc - ref_itc)) <= (1e-13 if dtype == 'float64' else 1e-5)
+    np.testing.assert_allclose(other.execute(x, out_kind='phase_sum'), plan.execute(x, out_kind='phase_sum'),
+                               rtol=1e-13, atol=1e-13 * S)
+    o = oracle('morse', x, freqs[::51], 'cwt')
+    pm = plan.execute(x, out_kind='power_mean')
+    assert within(pm[::51], np.mean(np.abs(o) ** 2, axis=0), dtype, 'power')
+    t_itc = 1e-10 if dtype == 'float64' else 1e-4
+    assert np.max(np.abs(itc[::51] - np.abs(np.mean(o / np.abs(o), axis=0)))) <= t_itc

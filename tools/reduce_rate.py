@@ -1,6 +1,6 @@
 """Epoch reductions vs the per-signal output on device tensors (the library given by
 NINWAVE_LIB): power_mean / itc against power, 512 signals x 256 scales, per n and dtype.
-    DTYPES="float64 float32" NS="1024 2048 4096" python tools/reduce_rate.py [tag]"""
+    DTYPES="float64 float32" NS="1024 2048 4096 1201" python tools/reduce_rate.py [tag]"""
 import os, sys, time
 import numpy as np
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
