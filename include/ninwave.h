@@ -36,6 +36,7 @@ extern "C" {
 #define NW_E_NOMEM        -4   /* device allocation failed */
 #define NW_E_STATE        -5   /* call out of order (e.g. execute before set_wavelet) */
 #define NW_E_NODEVICE     -6   /* no HIP device visible */
+#define NW_E_BOUNDS       -7   /* debug library only: a kernel bounds check failed */
 
 /* compute dtypes (the arithmetic type of the whole path) */
 #define NW_F32 0
@@ -133,6 +134,16 @@ typedef struct nw_plan nw_plan;
 
 const char* nw_last_error(void);
 const char* nw_version(void);
+/* Diagnostics on stderr ("[ninwave] ..." lines): 0 silent, 1 plan / engine / reduction-path
+ * decisions and every error status, 2 also every launch stage (and its time under NW_TIMING).
+ * Default: the NW_LOG environment variable, else 0.  Returns the previous level. */
+int nw_set_log_level(int level);
+/* 1 in the debug library (libninwave_debug.so: kernel bounds checks, every call synchronous,
+ * NW_E_BOUNDS names the failing file:line), 0 in the product library. */
+int nw_debug_bounds(void);
+/* Debug library: launches one kernel whose checks fail on purpose (no memory is touched) and
+ * returns the resulting NW_E_BOUNDS status; the product library returns NW_E_STATE. */
+int nw_debug_selftest(int device);
 int nw_device_count(int* n);
 
 /* Host-only (no GPU): the grid of the reference's make_fft_wavelet(freq, real_length)

@@ -24,6 +24,7 @@ NW_E_ROCFFT = -3
 NW_E_NOMEM = -4
 NW_E_STATE = -5
 NW_E_NODEVICE = -6
+NW_E_BOUNDS = -7
 
 NW_F32, NW_F64 = 0, 1
 NW_MORSE, NW_MORLET, NW_SHANNON, NW_TABLE = 1, 2, 3, 4
@@ -68,6 +69,9 @@ _I64 = ctypes.c_int64
 SIGNATURES = [
     ('nw_last_error', ctypes.c_char_p, []),
     ('nw_version', ctypes.c_char_p, []),
+    ('nw_set_log_level', ctypes.c_int, [ctypes.c_int]),
+    ('nw_debug_bounds', ctypes.c_int, []),
+    ('nw_debug_selftest', ctypes.c_int, [ctypes.c_int]),
     ('nw_device_count', ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     ('nw_trans_grid', ctypes.c_int, [ctypes.c_double, ctypes.c_double, ctypes.c_int, ctypes.POINTER(nw_grid)]),
     ('nw_fused_supported', ctypes.c_int, [_I64, ctypes.c_int]),
@@ -132,6 +136,12 @@ def check(rc):
         if rc == NW_E_INVALID:
             raise ValueError(msg)
         raise NinwaveError(rc, msg)
+
+
+def set_log_level(level: int) -> int:
+    """NW_LOG diagnostics on stderr (0 silent, 1 decisions and errors, 2 every launch); returns
+    the previous level."""
+    return int(lib().nw_set_log_level(int(level)))
 
 
 def device_count() -> int:

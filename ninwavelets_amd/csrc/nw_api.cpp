@@ -10,8 +10,11 @@
 #include <rocfft/rocfft.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -20,14 +23,56 @@
 #include <unordered_map>
 #include <vector>
 
+#include "nw_dcheck.h"
 #include "nw_internal.h"
 
 namespace {
 
 thread_local std::string g_last_error;
 
+// NW_LOG (SURVEY.md §5 "Metrics / logging"; the reference only prints SizeError, base.py:71-72):
+// 0 = silent (default), 1 = plan / engine / reduction-path decisions and every error status,
+// 2 = also every launch stage with its kernel and, under NW_TIMING, its time.  Read from the
+// environment at first use; nw_set_log_level() overrides it.  One line per event on stderr.
+std::atomic<int> g_log_level{-1};
+std::mutex g_log_mu;
+
+int log_level() {
+    int l = g_log_level.load(std::memory_order_relaxed);
+    if (l >= 0) return l;
+    const char* s = std::getenv("NW_LOG");
+    int expect = -1;
+    g_log_level.compare_exchange_strong(expect, s ? std::max(0, std::atoi(s)) : 0);
+    return g_log_level.load();
+}
+
+__attribute__((format(printf, 2, 3))) void nw_logf(int level, const char* fmt, ...) {
+    if (log_level() < level) return;
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    std::lock_guard<std::mutex> g(g_log_mu);
+    std::fprintf(stderr, "[ninwave] %s\n", buf);
+}
+
+const char* out_name(int k) {
+    static const char* names[] = {"cwt", "abs", "power", "power_mean", "itc", "power_sum", "phase_sum"};
+    if (k == 1001) return "power partials";
+    if (k == 1002) return "phase partials";
+    return k >= 0 && k < 7 ? names[k] : "?";
+}
+const char* kernel_name(int64_t k) {
+    static const char* names[] = {"none", "nw_fused_kernel", "nw_fused_pair_kernel", "nw_chirp_kernel",
+                                  "rows_kernel + cols_kernel", "k1_multiply + rocFFT"};
+    return k >= 0 && k < 6 ? names[k] : "?";
+}
+const char* dtype_name(int dt) { return dt == NW_F32 ? "float32" : "float64"; }
+
 int fail(int code, const std::string& msg) {
     g_last_error = msg;
+    nw_logf(1, "error %d: %s", code, msg.c_str());
     return code;
 }
 
@@ -66,7 +111,41 @@ struct DeviceGuard {
     }
 };
 
+// debug library: every kernel file's check words (nw_dcheck.h), read and cleared after each
+// synchronising call; the product library registers none
+std::vector<nw::DcheckTake>& dcheck_registry() {
+    static std::vector<nw::DcheckTake> r;
+    return r;
+}
+
+#ifdef NW_DEBUG_BOUNDS
+constexpr bool kDebugBounds = true;
+#else
+constexpr bool kDebugBounds = false;
+#endif
+
+// after the device's work is complete: NW_E_BOUNDS if any kernel check failed since the last call
+int dcheck_collect(hipStream_t stream) {
+    if (!kDebugBounds) return NW_OK;
+    hipError_t e = stream ? hipStreamSynchronize(stream) : hipDeviceSynchronize();
+    if (e != hipSuccess) return fail(NW_E_HIP, std::string("synchronize: ") + hipGetErrorString(e));
+    std::string msg;
+    for (nw::DcheckTake take : dcheck_registry()) {
+        unsigned fails = 0, site = 0;
+        const char* file = "";
+        e = take(&fails, &site, &file);
+        if (e != hipSuccess) return fail(NW_E_HIP, std::string("bounds-check readback: ") + hipGetErrorString(e));
+        if (!fails) continue;
+        std::string where = site >= nw::kDcheckHeaderSite
+                                ? "nw_fft_dev.h:" + std::to_string(site - nw::kDcheckHeaderSite)
+                                : std::string(file) + ":" + std::to_string(site);
+        msg += (msg.empty() ? "" : "; ") + std::to_string(fails) + " failing check(s), first at " + where;
+    }
+    return msg.empty() ? NW_OK : fail(NW_E_BOUNDS, "kernel bounds check: " + msg);
+}
+
 enum Stage { ST_FWD = 0, ST_MUL, ST_INV, ST_EPI, ST_FUSED, ST_COPY, ST_ROWS, ST_EXPAND, ST_N };
+const char* const kStageName[ST_N] = {"forward", "multiply", "inverse", "epilogue", "fused", "copy", "rows", "expand"};
 
 struct Pending {
     int stage;
@@ -199,6 +278,8 @@ void count_launch(nw_plan* p, int stage) {
 template <typename F>
 int staged(nw_plan* p, int stage, F&& fn) {
     count_launch(p, stage);
+    nw_logf(2, "plan %p: launch %s%s%s", (void*)p, kStageName[stage], stage == ST_FUSED || stage == ST_ROWS ? ": " : "",
+            stage == ST_FUSED || stage == ST_ROWS ? kernel_name(p->stats.kernel) : "");
     if (!(p->flags & NW_TIMING)) return fn();
     Pending pe{stage, nullptr, nullptr};
     NW_TRY(take_event(p, &pe.a));
@@ -216,6 +297,7 @@ int resolve_timing(nw_plan* p) {
     for (const Pending& pe : p->pending) {
         float ms = 0.f;
         NW_HIP(hipEventElapsedTime(&ms, pe.a, pe.b));
+        nw_logf(2, "plan %p: %s %.3f ms", (void*)p, kStageName[pe.stage], ms);
         switch (pe.stage) {
             case ST_FWD: p->stats.ms_forward += ms; break;
             case ST_MUL: p->stats.ms_multiply += ms; break;
@@ -364,9 +446,12 @@ int chirp_table(nw_plan* p) {
             p->chirp = false;
             p->engine = NW_ENGINE_ROCFFT;
             p->stats.engine = NW_ENGINE_ROCFFT;
+            nw_logf(1, "plan %p: no wavelet row fits the on-chip chirp-z transform: rocFFT engine", (void*)p);
             return NW_OK;
         }
         NW_TRY(build_overflow_view(p, over));
+        nw_logf(1, "plan %p: chirp-z form, %d of %d rows too wide for the chip run through rocFFT (hybrid)",
+                (void*)p, (int)over.size(), p->nfreq);
     }
     p->wtab_valid = true;
     return NW_OK;
@@ -605,6 +690,9 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     const bool psum = (fused && !p->large && !p->chirp &&
                        nw::fused_psum_supported(p->n, p->dtype, p->desc.kind, phase)) || chirp_psum;
     const int sig_kind = psum ? (phase ? OUT_PHSUM : OUT_PSUM) : (fused && !phase) ? NW_OUT_POWER : NW_OUT_CWT;
+    nw_logf(1, "plan %p: %s over %lld signals: %s", (void*)p, out_name(out_kind), (long long)nsig,
+            psum ? "fp64 block partial sums inside the transform kernel"
+                 : "per-signal rows per chunk, added in signal order in fp64");
     // partials: plain fp64 sums (phase partials as 2 fn reals)
     const int src_kind = psum ? nw::ACC_POWER_REAL
                               : phase ? nw::ACC_PHASE_Y : (fused ? nw::ACC_POWER_REAL : nw::ACC_POWER_Y);
@@ -710,11 +798,37 @@ void free_plan(nw_plan* p) {
 
 }  // namespace
 
+namespace nw {
+int dcheck_register(DcheckTake fn) {
+    dcheck_registry().push_back(fn);
+    return (int)dcheck_registry().size();
+}
+}  // namespace nw
+
 extern "C" {
 
 const char* nw_last_error(void) { return g_last_error.c_str(); }
 
 const char* nw_version(void) { return "ninwave 0.1.0 (gfx950)"; }
+
+int nw_debug_bounds(void) { return kDebugBounds ? 1 : 0; }
+
+int nw_debug_selftest(int device) {
+    if (!kDebugBounds) return fail(NW_E_STATE, "nw_debug_selftest: not the debug library");
+    int ndev = 0;
+    NW_TRY(nw_device_count(&ndev));
+    if (device < 0 || device >= ndev) return fail(NW_E_INVALID, "nw_debug_selftest: device out of range");
+    DeviceGuard guard(device);
+    NW_TRY(dcheck_collect(nullptr));   // nothing pending from earlier calls
+    NW_HIP(nw::launch_dcheck_selftest(nullptr));
+    return dcheck_collect(nullptr);
+}
+
+int nw_set_log_level(int level) {
+    const int prev = log_level();
+    g_log_level.store(std::max(0, level));
+    return prev;
+}
 
 int nw_device_count(int* n) {
     if (!n) return fail(NW_E_INVALID, "nw_device_count: null pointer");
@@ -804,6 +918,13 @@ int nw_plan_create(nw_plan** out, int device, int64_t n, int64_t max_batch, int3
         e = nw::fused_prepare(n, dtype);
         if (e != hipSuccess) return bail(fail(NW_E_HIP, std::string("fused_prepare: ") + hipGetErrorString(e)));
     }
+    nw_logf(1, "plan %p: device %d n %lld nfreq %d %s max_batch %lld: %s engine, %s", (void*)p, device, (long long)n,
+            (int)nfreq, dtype_name(dtype), (long long)max_batch,
+            p->engine == NW_ENGINE_FUSED ? "fused" : "rocFFT",
+            p->engine == NW_ENGINE_ROCFFT ? "rocFFT forward / K1 multiply / rocFFT inverse / K2 epilogue"
+            : p->large ? "two-pass form (rows_kernel + cols_kernel)"
+            : p->chirp_tentative ? "chirp-z form if every row fits on chip (settled at the first execute)"
+            : p->chirp ? "chirp-z form (nw_chirp_kernel)" : "one-pass form (fwd_r2c_kernel + nw_fused_kernel)");
     *out = p;
     return NW_OK;
 }
@@ -1052,7 +1173,12 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
         p->engine = NW_ENGINE_FUSED;
         p->stats.engine = NW_ENGINE_FUSED;
     }
-    return setup_unique_rows(p, kind, freqs, peak, xstep, normal ? nullptr : table);
+    NW_TRY(setup_unique_rows(p, kind, freqs, peak, xstep, normal ? nullptr : table));
+    nw_logf(1, "plan %p: wavelet kind %d, %d scales (%s), row length %lld", (void*)p, kind, F,
+            p->dedup ? (std::to_string(p->nuniq) + " distinct rows, expanded after the transform").c_str()
+                     : "every row distinct",
+            (long long)d.len_full);
+    return NW_OK;
 }
 
 int nw_plan_wavelet_shape(nw_plan* p, int64_t* len_full, int64_t* row_len) {
@@ -1106,7 +1232,12 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
         }
     }
 
-    if (is_reduction(out_kind)) return execute_reduce(p, x, nsig, out, out_kind, mem == NW_MEM_HOST);
+    nw_logf(1, "plan %p: execute %s, %lld signals, %s buffers", (void*)p, out_name(out_kind), (long long)nsig,
+            mem == NW_MEM_HOST ? "host" : "device");
+    if (is_reduction(out_kind)) {
+        NW_TRY(execute_reduce(p, x, nsig, out, out_kind, mem == NW_MEM_HOST));
+        return dcheck_collect(p->stream);
+    }
 
     const size_t out_elem = (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
     const size_t row_out = (size_t)p->nfreq * p->n * out_elem;  // one signal's output bytes
@@ -1137,7 +1268,7 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     }
     p->stats.executes++;
     if (host) NW_TRY(resolve_timing(p));
-    return NW_OK;
+    return dcheck_collect(p->stream);
 }
 
 }  // extern "C"
@@ -1414,7 +1545,7 @@ int nw_baseline(int device, int dtype, const void* x, int64_t count, int64_t row
         if (dx) (void)hipFree(dx);
         if (dout) (void)hipFree(dout);
     }
-    return rc;
+    return rc == NW_OK ? dcheck_collect(nullptr) : rc;
 }
 
 int nw_make_wavelets(int device, int kind, const double* params, int nparams, const double* freqs, int nfreq,
@@ -1530,7 +1661,7 @@ int nw_make_wavelets(int device, int kind, const double* params, int nparams, co
     if (info) rocfft_execution_info_destroy(info);
     for (void* b : {d_rows, d_buf, d_out})
         if (b) (void)hipFree(b);
-    return rc;
+    return rc == NW_OK ? dcheck_collect(nullptr) : rc;
 }
 
 int nw_plan_set_stream(nw_plan* p, void* stream) {
@@ -1549,7 +1680,8 @@ int nw_plan_sync(nw_plan* p) {
     if (!p) return fail(NW_E_INVALID, "nw_plan_sync: null plan");
     DeviceGuard guard(p->device);
     NW_HIP(hipStreamSynchronize(p->stream));
-    return resolve_timing(p);
+    NW_TRY(resolve_timing(p));
+    return dcheck_collect(p->stream);
 }
 
 int nw_plan_stats(nw_plan* p, nw_stats* s) {

@@ -134,6 +134,8 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E, OUT>)) void nw_chirp_ker
     const float inv_n2 = 1.0f / (float)n2;
     const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * n;
     const int nz = (ksup[fi] + TT - 1) / TT;   // pass-0 elements reaching the support (<= E/2)
+    // the row's M class: wrap-free (M >= n + K - 1) and the pruned pass 0 (M >= 2K, nz <= E/2)
+    NW_DCHECK(fi >= 0 && fi < d.nfreq && s_end <= nsig && n + max(ksup[fi], 1) - 1 <= M && 2 * ksup[fi] <= M);
     Tab1<T, M, E>::fill(lds, tw, t);
     for (int64_t s = s_begin; s < s_end; ++s) {
         const cplx<T>* Xs = X + s * d.nh;

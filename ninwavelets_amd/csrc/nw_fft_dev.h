@@ -7,6 +7,7 @@
 
 #include <type_traits>
 
+#include "nw_dcheck.h"
 #include "nw_internal.h"
 
 // Tuning constants; each was measured against its alternatives (numbers in DESIGN.md §4).
@@ -347,6 +348,7 @@ __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
     using G = Geometry<N, E>;
     constexpr int PG = kPadX<T, N, E, P + 1>;
     if constexpr (P == 0) {
+        NW_DCHECK_H(lds_idx_p<PG>(t * E + E - 1) < kImgElems<T, N, E>);
         Pair<T>* dst = reinterpret_cast<Pair<T>*>(lds + lds_idx_p<PG>(t * E));
 #pragma unroll
         for (int u = 0; u < E / 2; ++u)
@@ -359,6 +361,7 @@ __device__ __forceinline__ void lds_write(C2<T>* v, T* lds, int t) {
         for (int q = 0; q < Q; ++q) {
             // lane-contiguous butterflies (OSZ 16: never the paired last-pass order), or pass 1's remap
             const int j = PassInfo<N, E, P, 16, kIsPair<T>>::bfly(t, q);
+            NW_DCHECK_H(lds_idx_p<PG>((j / NS) * NS * R + j % NS) + lds_off_p<PG>((R - 1) * NS) < kImgElems<T, N, E>);
             T* dst = lds + lds_idx_p<PG>((j / NS) * NS * R + j % NS);
 #pragma unroll
             for (int i = 0; i < R; ++i) dst[lds_off_p<PG>(bitrev<R>(i) * NS)] = comp<COMP>(v[q * R + i]);
@@ -434,6 +437,7 @@ __device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
     constexpr int R = I::R, Q = I::Q;
     constexpr int PG = kPadX<T, N, E, P>;
     if constexpr (I::PAIRED) {
+        NW_DCHECK_H(lds_idx_p<PG>(I::bfly(t, 0)) + (Q - 1) + lds_off_p<PG>((R - 1) * I::STRIDE) < kImgElems<T, N, E>);
         const T* src = lds + lds_idx_p<PG>(I::bfly(t, 0));
 #pragma unroll
         for (int q = 0; q < Q; q += 2)
@@ -446,6 +450,7 @@ __device__ __forceinline__ void lds_read(C2<T>* v, const T* lds, int t) {
     } else {
 #pragma unroll
         for (int q = 0; q < Q; ++q) {
+            NW_DCHECK_H(lds_idx_p<PG>(I::bfly(t, q)) + lds_off_p<PG>((R - 1) * I::STRIDE) < kImgElems<T, N, E>);
             const T* src = lds + lds_idx_p<PG>(I::bfly(t, q));
 #pragma unroll
             for (int r = 0; r < R; ++r) comp<COMP>(v[q * R + r]) = src[lds_off_p<PG>(r * I::STRIDE)];
@@ -588,6 +593,7 @@ struct LastStores {
         constexpr int q = (K / R) * STEP, i = K % R;
         const uint32_t lane = (uint32_t)I::bfly(t, 0);        // Q*t (paired) or t
         constexpr uint32_t c = (uint32_t)((I::PAIRED ? q : q * Geometry<N, E>::T) + bitrev<R>(i) * I::NS);
+        NW_DCHECK_H(lane + c + (I::PAIRED ? 1u : 0u) < (uint32_t)N);
         if constexpr (I::PAIRED)
             store_pair<OUT, T>(orow, lane, c, o[q * R + i], o[(q + 1) * R + i]);
         else

@@ -181,6 +181,7 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     // exactly-zero W for every thread of the block (k = t + r*T beyond the row's last
     // nonzero bin), so they are neither read nor multiplied and the DIF stages skip them
     const int nz = max(1, wnz[fi] >> WSH);
+    NW_DCHECK(fi < d.nfreq && s_end <= nsig && d.n == N && nz <= E);
     // LDS-DMA only the X bins the pruned pass 0 reads: variant NZ (>= 4) reads bins < NZ*T,
     // i.e. NZ/2 rounds of 2*T bins, when it reads no mirrored bin (NZ <= E/2)
     const int nzv = nz < kPruneMin ? kPruneMin : nz;
@@ -313,6 +314,7 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
     Tab1<f2, N, E>::fill(lds, tw, t);
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<float>) : sizeof(float));
     const int nz = wnz[fi];
+    NW_DCHECK(fi < d.nfreq && s_end <= nsig && d.n == N && nz >= 1 && nz <= E);
     auto xrow = [&](int64_t s) { return reinterpret_cast<const C2<float>*>(X + s * d.nh); };
     // power partial sums (kOutPSum): as nw_fused_kernel, both signals of a pair into one sum
     constexpr bool PSUM = OUT == kOutPSum;

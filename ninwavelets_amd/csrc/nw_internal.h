@@ -129,6 +129,8 @@ hipError_t launch_epilogue(int dtype, int out_kind, const void* Y, void* out, in
 hipError_t launch_rows(const WDesc& d, int dtype, void* rows, hipStream_t s);
 // repeated rows: dst (nsig, nf, row) from src (nsig, nu, row), scales grouped by distinct row
 hipError_t launch_gather(const void* src, void* dst, const int32_t* idx, int count, size_t elem_bytes, hipStream_t s);
+// debug library: one 64-lane block whose lanes >= 32 fail an NW_DCHECK (no memory access)
+hipError_t launch_dcheck_selftest(hipStream_t s);
 hipError_t launch_expand_rows(const void* src, void* dst, int64_t nsig, int nu, int nf, size_t row_bytes,
                               const int32_t* offs, const int32_t* order, hipStream_t s);
 // epoch reductions: source kinds of launch_accumulate

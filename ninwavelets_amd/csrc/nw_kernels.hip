@@ -14,6 +14,7 @@
 // amortised over the group.  Stores are 16 B per lane (float4 / double2).
 #include <type_traits>
 
+#include "nw_dcheck.h"
 #include "nw_internal.h"
 
 namespace nw {
@@ -494,7 +495,11 @@ __global__ __launch_bounds__(256) void k_expand_rows(const V* __restrict__ src, 
         const V v = src[su * rowv + k];
         V* base = dst + (su / nu) * nf * rowv + k;
         const int i1 = offs[u + 1];
-        for (int i = offs[u]; i < i1; ++i) __builtin_nontemporal_store(v, base + (int64_t)order[i] * rowv);
+        NW_DCHECK(offs[u] <= i1 && i1 <= nf);
+        for (int i = offs[u]; i < i1; ++i) {
+            NW_DCHECK(order[i] >= 0 && order[i] < nf);
+            __builtin_nontemporal_store(v, base + (int64_t)order[i] * rowv);
+        }
     }
 }
 
@@ -507,6 +512,13 @@ __global__ __launch_bounds__(256) void k_gather_elems(const uint32_t* __restrict
         const int64_t i = g / words, w = g - i * words;
         dst[g] = src[(int64_t)idx[i] * words + w];
     }
+}
+
+__global__ __launch_bounds__(64) void k_dcheck_selftest(int n) { NW_DCHECK((int)threadIdx.x < n); }
+
+hipError_t launch_dcheck_selftest(hipStream_t s) {
+    k_dcheck_selftest<<<1, 64, 0, s>>>(32);
+    return hipGetLastError();
 }
 
 hipError_t launch_gather(const void* src, void* dst, const int32_t* idx, int count, size_t elem_bytes, hipStream_t s) {

@@ -224,6 +224,7 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
     if (fl >= nf || rg >= ngroups) return;
     const int fi = f0 + fl;
     const int km = kmax[fi];
+    NW_DCHECK(fi < d.nfreq && (rg + 1) * rgs <= n1 && (int64_t)n1 * N2 == d.n && km < d.n);
     RowW<T, KIND> wf;
     if constexpr (KIND != NW_TABLE) wf.init(d, fi);
 

@@ -147,3 +147,50 @@ def test_reference_api_surface():
     nu = np.linspace(0, 500, 1001)
     np.testing.assert_array_equal(nw.Morse().trans_formula(nu, 40.), O.morse_spectrum(nu, 40.))
     np.testing.assert_array_equal(nw.Morlet().trans_formula(nu, 40.), O.morlet_spectrum(nu, 40.))
+
+
+def test_nw_log_levels():
+    """NW_LOG: errors are reported on stderr at level >= 1, silent at 0; the
+    environment sets the default, nw_set_log_level overrides it."""
+    import subprocess
+    import sys
+    code = ('import ctypes, sys; sys.path.insert(0, %r)\n'
+            'from ninwavelets_amd import _lib as L\n'
+            'p = ctypes.c_void_p()\n'
+            'prev = L.set_log_level(0); L.set_log_level(prev); print("level", prev, flush=True)\n'
+            'L.set_log_level(int(sys.argv[1]))\n'
+            'rc = L.lib().nw_plan_create(ctypes.byref(p), 0, 0, 1, 1, 1, 0)\n'
+            'print("rc", rc, flush=True)\n') % ROOT
+    for env_level, set_level, expect in (('1', 1, True), ('0', 0, False), ('1', 0, False), ('0', 2, True)):
+        env = dict(os.environ, NW_LOG=env_level)
+        r = subprocess.run([sys.executable, '-c', code, str(set_level)], capture_output=True, text=True, env=env,
+                           timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert f'level {env_level}' in r.stdout and f'rc {L.NW_E_INVALID}' in r.stdout
+        logged = [ln for ln in r.stderr.splitlines() if ln.startswith('[ninwave] error')]
+        assert bool(logged) == expect, r.stderr
+        if expect:
+            assert 'n, max_batch, nfreq must be >= 1' in logged[0]
+
+
+def test_debug_library_builds_and_exports():
+    """libninwave_debug.so (kernel bounds checks) exports the same header; the product library
+    reports no checks and refuses the self-test."""
+    import subprocess
+    import sys
+    dbg = os.path.join(ROOT, 'ninwavelets_amd', 'libninwave_debug.so')
+    assert os.path.exists(dbg), 'make -C ninwavelets_amd/csrc debug'
+    code = ('import sys; sys.path.insert(0, %r)\n'
+            'from ninwavelets_amd import _lib as L\n'
+            'lib = L.lib()\n'
+            'print(lib.nw_debug_bounds(), lib.nw_debug_selftest(0) if not sys.argv[1:] else "-")\n') % ROOT
+    r = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120,
+                       env=dict(os.environ, NINWAVE_LIB=dbg))
+    assert r.returncode == 0, r.stderr
+    bounds, _ = r.stdout.split()
+    assert bounds == '1'
+    lib = ctypes.CDLL(dbg)
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    assert L.lib().nw_debug_bounds() == 0
+    assert L.lib().nw_debug_selftest(0) == L.NW_E_STATE

@@ -8,7 +8,10 @@ that runtime:
   1. every single-signal reference golden (tests/golden/*.npz), fp64 and fp32, both engines;
   2. the reference's outputs at the benchmark lengths (tests/golden/long_*.npz), fp64 and fp32;
   3. the C3 / C4 bench shapes: Morse power at N = 4096 (nw_fused_pair_kernel) and N = 16384
-     (nw_fused_kernel), all 256 scales of 4 signals, against the oracle.
+     (nw_fused_kernel), all 256 scales of 4 signals, against the oracle;
+  4. epoch power_mean / itc on each engine form against the same plan's per-signal outputs.
+With NINWAVE_LIB naming the debug library (tests/test_gpu_debug.py) the same run exercises
+the kernel bounds checks: a failing check is an NW_E_BOUNDS error in the case that hit it.
 Tolerances are tests/test_gpu_parity.py's (fp64 1e-12, fp32 1e-5 of max|ref|, x2 for |.|^2,
 1e-4 for fp32 at N >= 2^17).  Prints one JSON summary line; exits 1 on any failure.
 """
@@ -32,7 +35,7 @@ from ninwavelets_amd import _lib as L  # noqa: E402
 CLASSES = {'morse': nw.Morse, 'morlet': nw.Morlet, 'shannon': nw.Shannon,
            'mexican_hat': nw.MexicanHat, 'haar': nw.Haar}
 TOL = {'float64': 1e-12, 'float32': 1e-5}
-failures, counts = [], {'single': 0, 'long': 0, 'bench_shapes': 0}
+failures, counts = [], {'single': 0, 'long': 0, 'bench_shapes': 0, 'reductions': 0}
 
 
 def close(got, ref, rtol, dtype):
@@ -104,6 +107,31 @@ def bench_shapes():
         plan.close()
 
 
+def reductions():
+    """Epoch reductions on every engine form (fused partials incl. the pair kernel, chirp-z
+    partials, the two-pass chunk path): power_mean / itc against the same plan's per-signal
+    power / cwt (mneutils.py:42-71)."""
+    rng = np.random.default_rng(5)
+    freqs = np.arange(1, 257, 16, dtype=np.float64)
+    for n, dtype in ((1201, 'float32'), (1201, 'float64'), (4096, 'float32'), (4096, 'float64'),
+                     (16384, 'float32'), (32768, 'float32')):
+        x = rng.standard_normal((11, n)).astype(dtype)
+        g = L.trans_grid(n / 1000., 1000., False)
+        plan = nw.Plan(n, len(freqs), dtype, max_batch=4)
+        plan.set_wavelet('morse', [17.5, 3.], freqs, g)
+        pw = plan.execute(x, out_kind='power').astype(np.float64)
+        y = plan.execute(x, out_kind='cwt').astype(np.complex128)
+        pm = plan.execute(x, out_kind='power_mean')
+        itc = plan.execute(x, out_kind='itc')
+        plan.close()
+        f32 = dtype == 'float32'
+        counts['reductions'] += 1
+        e_pm = rel(pm, pw.mean(axis=0))
+        e_itc = np.max(np.abs(itc - np.abs(np.mean(y / np.abs(y), axis=0))))
+        if e_pm > (1e-5 if f32 else 1e-12) or e_itc > (1e-4 if f32 else 1e-10):
+            failures.append(('reduction', n, dtype, e_pm, e_itc))
+
+
 def hip_runtime_path():
     with open('/proc/self/maps') as f:
         libs = sorted({ln.split()[-1] for ln in f if 'libamdhip64' in ln or 'librocfft' in ln})
@@ -113,7 +141,9 @@ def hip_runtime_path():
 single_goldens()
 long_goldens()
 bench_shapes()
+reductions()
 summary = {'torch_imported': 'torch' in sys.modules, 'runtime': hip_runtime_path(), 'counts': counts,
+           'lib': L.LIB_PATH, 'debug_bounds': int(L.lib().nw_debug_bounds()),
            'failures': [list(map(str, f)) for f in failures]}
 print(json.dumps(summary), flush=True)
 sys.exit(1 if failures or summary['torch_imported'] else 0)
