@@ -77,6 +77,7 @@ __device__ __forceinline__ C2<T> chirp(int k, uint32_t n2, float inv_n2, const C
         const float rev = (float)m * inv_n2;
         return C2<T>{__builtin_amdgcn_cosf(rev), __builtin_amdgcn_sinf(rev)};
     } else {
+        NW_DCHECK(k >= 0 && (uint32_t)k < n2 / 2);
         return ct[k];
     }
 }
@@ -201,7 +202,9 @@ __global__ __launch_bounds__(M / E, (kChirpWps<T, M, E, OUT>)) void nw_chirp_ker
                 const int i = bitrev<IL::R>(j);
                 const int idx = (int)n0 + j * IL::NS;
                 C2<T> y = v[q * IL::R + i];
-                if constexpr (EPI) y = cmul(y, chirp<T>(idx, n2, inv_n2, ct));
+                // (idx >= n: not stored; the chirp index is clamped so the fp64 table ct[0 .. n)
+                // is never read past its end, whatever the compiler hoists)
+                if constexpr (EPI) y = cmul(y, chirp<T>(idx < n ? idx : 0, n2, inv_n2, ct));
                 if constexpr (OUT == kOutPSum) {
                     // the power output's own value (out_value), added in fp64 like k_accumulate
                     const double pv = (double)out_value<NW_OUT_POWER, T>(y);

@@ -269,11 +269,44 @@ __device__ __forceinline__ typename OutT<OUT, T>::type out_value(C2<T> y) {
     else return (T)sqrt(y.re * y.re + y.im * y.im);
 }
 
+// Output store policies (each kernel picks one; measured with tools/ab.sh on one box):
+//   kStoreGlobal: global stores, streaming (nt) for paired / packed outputs, plain for the
+//     16-B unpaired ones (fp32 C4 3.364 ms; nt there too 3.36; the C5 passes);
+//   kStoreGlobalNt: global nt for every output (fp64 C4 shape 9.14-9.34 -> 8.29-8.40 ms per
+//     launch, the C5 fp64 row pass: plain 16-B complex128 stores were the slow ones);
+//   kStoreBuffer: raw buffer nt stores, the compile-time offset in the descriptor base (scalar
+//     adds instead of per-store VGPR address adds): the signal-pair kernel, C3 1.268 -> 1.222 ms
+//     (fp32 C4 3.364 -> 3.402, the C5 fp64 row pass 0.93 -> 1.06 and the chirp-z kernel
+//     1.23 -> 1.44 ms were slower with it).
+// The buffer form keeps the descriptor's SGPR offset field 0: with a register there, a VALU
+// write of the store's data VGPRs in the very next instruction (which the compiler does not
+// guard for that form) corrupted the first dword of 16-B stores on gfx950.
+constexpr int kStoreGlobal = 0, kStoreGlobalNt = 1, kStoreBuffer = 2;
+template <int SP, typename V>
+__device__ __forceinline__ void store_row(V val, void* row, uint32_t lane_off, uint32_t c_off) {
+    if constexpr (SP == kStoreBuffer) {
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(row) + c_off, 0, 0x7fffffff, 0x00020000);
+        if constexpr (sizeof(V) == 16)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, val),
+                                                   rs, (int)lane_off, 0, 2);
+        else if constexpr (sizeof(V) == 8)
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, val),
+                                                  rs, (int)lane_off, 0, 2);
+        else
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs, (int)lane_off, 0, 2);
+    } else {
+        __builtin_nontemporal_store(val, reinterpret_cast<V*>(at(reinterpret_cast<char*>(row), lane_off, c_off)));
+    }
+}
+template <typename O> using StoreVec =
+    typename std::conditional<sizeof(O) == 16, float __attribute__((ext_vector_type(4))),
+    typename std::conditional<sizeof(O) == 8, float __attribute__((ext_vector_type(2))), float>::type>::type;
+
 // store outputs idx, idx+1 of the current row (orow: wave-uniform row base) as ONE
 // vector store (16 B for complex64, 8 B for float32, 2x16 B for complex128)
 // outputs lane_idx + c_idx (pair: and the next one) of the current row
-// streaming (nt) stores: measured 5 % faster than plain at n = 16384
-template <int OUT, typename T>
+template <int OUT, typename T, int SP>
 __device__ __forceinline__ void store_pair(void* orow, uint32_t lane_idx, uint32_t c_idx, C2<T> y0, C2<T> y1) {
     using O = typename OutT<OUT, T>::type;
     struct alignas(2 * sizeof(O)) P2 { O a, b; };
@@ -285,19 +318,21 @@ __device__ __forceinline__ void store_pair(void* orow, uint32_t lane_idx, uint32
               typename std::conditional<sizeof(P2) == 8, float __attribute__((ext_vector_type(2))),
                                         double __attribute__((ext_vector_type(4)))>::type>::type;
     const P2 pv{out_value<OUT, T>(y0), out_value<OUT, T>(y1)};
-    __builtin_nontemporal_store(__builtin_bit_cast(V, pv),
-                                reinterpret_cast<V*>(at(reinterpret_cast<P2*>(orow), lane_idx * (uint32_t)sizeof(O),
-                                                        c_idx * (uint32_t)sizeof(O))));
+    store_row<SP>(__builtin_bit_cast(V, pv), orow, lane_idx * (uint32_t)sizeof(O), c_idx * (uint32_t)sizeof(O));
 }
-template <int OUT, typename T>
+template <int OUT, typename T, int SP>
 __device__ __forceinline__ void store_one(void* orow, uint32_t lane_idx, uint32_t c_idx, C2<T> y) {
     using O = typename OutT<OUT, T>::type;
 #ifdef NW_ABL_NOSTORE
     asm volatile("" ::"v"(y.re), "v"(y.im), "v"(lane_idx));
     return;
 #endif
-    *at(reinterpret_cast<O*>(orow), lane_idx * (uint32_t)sizeof(O), c_idx * (uint32_t)sizeof(O)) =
-        out_value<OUT, T>(y);
+    if constexpr (SP == kStoreGlobal)
+        *at(reinterpret_cast<O*>(orow), lane_idx * (uint32_t)sizeof(O), c_idx * (uint32_t)sizeof(O)) =
+            out_value<OUT, T>(y);
+    else
+        store_row<SP>(__builtin_bit_cast(StoreVec<O>, out_value<OUT, T>(y)), orow, lane_idx * (uint32_t)sizeof(O),
+                      c_idx * (uint32_t)sizeof(O));
 }
 
 // ---- diagnostic phase stamps (NW_STAMPS builds only; never in the product build).
@@ -535,7 +570,7 @@ template <typename F> __device__ __forceinline__ void xpose2(C2<F>& a, C2<F>& b,
 // as ONE 16-B store -- 4x fewer store instructions for |y|^2 (fp32), 2x for y.  The
 // stores, not their bytes, limited these sizes (n = 4096: 2x the bytes of cwt over
 // power cost +20 % time).
-template <typename T, int N, int E, int OUT>
+template <typename T, int N, int E, int OUT, int SP = kStoreGlobal>
 struct LastStores {
     using O = typename OutT<OUT, T>::type;
     using I = PassInfo<N, E, Geometry<N, E>::npass() - 1, (int)sizeof(O)>;
@@ -576,10 +611,8 @@ struct LastStores {
 #ifdef NW_ABL_NOSTORE
                 asm volatile("" ::"v"(__builtin_bit_cast(V, pk)));
 #else
-                __builtin_nontemporal_store(
-                    __builtin_bit_cast(V, pk),
-                    reinterpret_cast<V*>(at(reinterpret_cast<P16*>(orow), lane,
-                                            (uint32_t)((q * Geometry<N, E>::T + g * PACK * I::NS) * sizeof(O)))));
+                store_row<SP>(__builtin_bit_cast(V, pk), orow, lane,
+                              (uint32_t)((q * Geometry<N, E>::T + g * PACK * I::NS) * sizeof(O)));
 #endif
             }
         }
@@ -595,9 +628,9 @@ struct LastStores {
         constexpr uint32_t c = (uint32_t)((I::PAIRED ? q : q * Geometry<N, E>::T) + bitrev<R>(i) * I::NS);
         NW_DCHECK_H(lane + c + (I::PAIRED ? 1u : 0u) < (uint32_t)N);
         if constexpr (I::PAIRED)
-            store_pair<OUT, T>(orow, lane, c, o[q * R + i], o[(q + 1) * R + i]);
+            store_pair<OUT, T, SP>(orow, lane, c, o[q * R + i], o[(q + 1) * R + i]);
         else
-            store_one<OUT, T>(orow, lane, c, o[q * R + i]);
+            store_one<OUT, T, SP>(orow, lane, c, o[q * R + i]);
     }
     // stores [C*COUNT/NCH, (C+1)*COUNT/NCH) -- one chunk of a deferred signal
     template <int C, int NCH, int K = C * COUNT / NCH>
@@ -659,7 +692,7 @@ template <typename T, int N, int E> constexpr int kLdsBytes =
 // T = f2 (signal pairs): every element carries two signals' values; twiddles and the Tab1
 // table stay scalar (shared), and the last pass stores the low halves to ocur and the high
 // halves to ocur2 (nullptr: an odd last signal, its high half is not stored).
-template <typename T, int N, int E, int OUT, int P, bool XD>
+template <typename T, int N, int E, int OUT, int P, bool XD, int SP = kStoreGlobal>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
                                             Stamps* st, void* ocur2 = nullptr, int dma_rounds = 1 << 30,
@@ -820,13 +853,13 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                     a[i] = C2<S>{v[i].re.x, v[i].im.x};
                     b[i] = C2<S>{v[i].re.y, v[i].im.y};
                 }
-                LastStores<S, N, E, OUT>::all(a, ocur, t);
-                if (ocur2) LastStores<S, N, E, OUT>::all(b, ocur2, t);
+                LastStores<S, N, E, OUT, SP>::all(a, ocur, t);
+                if (ocur2) LastStores<S, N, E, OUT, SP>::all(b, ocur2, t);
             } else {
-                LastStores<T, N, E, OUT>::all(v, ocur, t);
+                LastStores<T, N, E, OUT, SP>::all(v, ocur, t);
             }
         } else {
-            passes_from<T, N, E, OUT, P + 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, acc);
+            passes_from<T, N, E, OUT, P + 1, XD, SP>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, acc);
         }
     }
 }

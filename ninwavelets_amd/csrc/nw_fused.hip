@@ -245,7 +245,8 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
         void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
-        passes_from<T, N, E, OUT, 1, XD>(v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds,
+        passes_from<T, N, E, OUT, 1, XD, (sizeof(T) == 8 ? kStoreGlobalNt : kStoreGlobal)>(
+            v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds,
                                          PSUM ? acc : nullptr);
     }
     if constexpr (PSUM) {
@@ -342,7 +343,7 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
         else pass0.template operator()<E>();
         void* o1 = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;
         void* o2 = two ? (void*)((char*)out + (s2 * d.nfreq + fi) * (int64_t)N * out_esz) : nullptr;
-        passes_from<f2, N, E, OUT, 1, false>(v, lds, t, tw, nullptr, nullptr, o1, nullptr, o2, 1 << 30,
+        passes_from<f2, N, E, OUT, 1, false, kStoreBuffer>(v, lds, t, tw, nullptr, nullptr, o1, nullptr, o2, 1 << 30,
                                              PSUM ? acc : nullptr);
     }
     if constexpr (PSUM) {

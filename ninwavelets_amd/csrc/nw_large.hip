@@ -316,7 +316,9 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
             }
             in_lds = xs_next != nullptr;
         }
-        passes_from<T, N2, E, NW_OUT_CWT, 1, XD>(v, lds, t, tw, x, xs_next, orow, nullptr, nullptr, rounds_next);
+        // B rows stored nt (fp64: the 16-B complex128 stores; plain ones made the C5 fp64 step
+        // 129.4 ms against 125.3)
+        passes_from<T, N2, E, NW_OUT_CWT, 1, XD, kStoreGlobalNt>(v, lds, t, tw, x, xs_next, orow, nullptr, nullptr, rounds_next);
     }
 }
 
