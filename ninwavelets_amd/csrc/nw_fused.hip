@@ -64,8 +64,16 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
 // Tuning constants (each measured against its alternatives):
 // E = 32 kernels keep the first kWKeep32 elements of W in registers for the block (a row
 // pruned to NZ <= 16 then reads no W per signal): C4 0 / 8 / 16 -> 3.537 / 3.486 / 3.456 ms
-// per launch; fp64 has no registers to spare (4 and 8 measured +-0 / slower, with spills)
-constexpr int kWKeep32 = 16;
+// per launch; fp64 has no registers to spare (4 and 8 measured +-0 / slower, with spills);
+// n = 8192 (256-thread blocks) keeps 8: 16 spilled 12-16 B there
+constexpr int kWKeep32 = 16, kWKeep32Small = 8;
+// (W elements beyond kWKeep32 evaluated in registers for Morse rows instead of re-read:
+// C4 3.360-3.368 -> 3.420-3.430 ms per launch; removing those loads altogether (diagnostic)
+// 3.367-3.369: the re-read costs nothing, the evaluation's VALU does)
+// E = 32: a pass-0 variant for rows whose support ends below 3/4 of n (NZ = 24: C4's rows
+// above 186 Hz), between the power-of-two variants: C4 3.360-3.368 -> 3.346-3.351 ms
+constexpr bool kNz24 = true;
+template <typename T, int N, int E> constexpr bool kNz24Of = kNz24 && E > 16;
 // signals per block: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (2 and 16 slower or equal).
 // fp64 (one block per CU) takes 4: an XCD round of 8 scales x 4 groups then reads W (8 x 128
 // KiB) + X (16 x 128 KiB) = 3 MiB, inside the XCD's 4 MiB L2 (8 signals: 5 MiB, re-read from
@@ -138,7 +146,7 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     // E = 32: the first WKEEP elements of W stay in registers for the block (a row pruned to
     // NZ <= WKEEP reads no W per signal; loads issued after the previous signal's stores
     // wait for all of them in the in-order vmcnt queue)
-    constexpr int WKEEP = (!WREG && REALW && sizeof(T) == 4) ? kWKeep32 : 0;
+    constexpr int WKEEP = (!WREG && REALW && sizeof(T) == 4) ? (N >= 16384 ? kWKeep32 : kWKeep32Small) : 0;
     WT wk[WKEEP > 0 ? WKEEP : 1];
     if constexpr (WKEEP > 0) {
 #pragma unroll
@@ -238,6 +246,7 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
         if (nz <= 4) pass0.template operator()<4>();
         else if (nz <= 8) pass0.template operator()<8>();
         else if (E > 16 && nz <= 16) pass0.template operator()<(E > 16 ? 16 : E)>();
+        else if (kNz24Of<T, N, E> && nz <= 24) pass0.template operator()<(E > 16 ? 24 : E)>();
         else pass0.template operator()<E>();
         if constexpr (XD) {
             if (s + 1 < s_end) nyq = reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh)[N / 2];
@@ -397,9 +406,11 @@ __global__ __launch_bounds__(256) void wtable_kernel(WDesc d, void* wtab) {
         reinterpret_cast<C2<T>*>(wtab)[(int64_t)fi * d.n + k] = C2<T>{w.re, w.im};
 }
 
-// Support of each W row for pass-0 pruning: wnz[f] = the smallest power of two >= the
-// number of pass-0 elements r (bins k = t + r*T, t < T) reaching the row's last nonzero
-// bin, i.e. elements r >= wnz[f] see W = 0 exactly for every thread.
+// Support of each W row for pass-0 pruning: wnz[f] >= the number of pass-0 elements r
+// (bins k = t + r*T, t < T) reaching the row's last nonzero bin, i.e. elements r >= wnz[f]
+// see W = 0 exactly for every thread: the next power of two up to 8, then the next multiple
+// of 8 (the pass-0 variants NZ = 4, 8, 16, 24, E; a multiple of 2^WSH, so nz >> WSH is exact
+// for the partial-sum kernels' smaller E).
 template <typename T, bool REALW>
 __global__ __launch_bounds__(256) void wsupport_kernel(const void* wtab, int64_t n, int tt, int e, int* wnz) {
     __shared__ int kmax[256];
@@ -423,7 +434,8 @@ __global__ __launch_bounds__(256) void wsupport_kernel(const void* wtab, int64_t
     if (threadIdx.x == 0) {
         const int need = kmax[0] < 0 ? 1 : kmax[0] / tt + 1;   // elements 0 .. need-1 can be nonzero
         int p2 = 1;
-        while (p2 < need) p2 <<= 1;
+        while (p2 < need && p2 < 8) p2 <<= 1;
+        if (p2 < need) p2 = kNz24 ? (need + 7) / 8 * 8 : [&] { int q = 8; while (q < need) q <<= 1; return q; }();
         wnz[fi] = p2 < e ? p2 : e;
     }
 }

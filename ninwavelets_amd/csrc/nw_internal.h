@@ -65,15 +65,22 @@ __device__ __forceinline__ double psi_f64(const WDesc& d, int fi, int64_t j) {
     }
 }
 
+// fp32 Morse psi at x = j * xstep (x > 0), in the log2 domain:
+// log2(psi/2) = b*log2(x) + (b/r)*log2(e)*(1 - x^r).  Contractions are explicit so the W
+// table (wtable_kernel), the two-pass row evaluator (RowW) and the fused kernel's in-register
+// W tail produce the same bits in every compilation context.
+__device__ __forceinline__ float morse_f32(float x, float b, float c1, float rr) {
+    const float lx = __log2f(x);
+    const float e2 = __builtin_fmaf(b, lx, c1 * (1.0f - exp2f(rr * lx)));   // the contraction clang chose for the plain expression
+    return 2.0f * exp2f(e2);
+}
+__device__ __forceinline__ float morse_c1_f32(const WDesc& d) { return (float)(d.b_over_r * 1.4426950408889634); }
+
 __device__ __forceinline__ float psi_f32(const WDesc& d, int fi, int64_t j) {
     if (d.kind == NW_MORSE) {
         const float x = (float)j * d.xstep32[fi];
         if (!(x > 0.0f)) return 0.0f;
-        const float lx = __log2f(x);
-        // log2(psi/2) = b*log2(x) + (b/r)*log2(e)*(1 - x^r)
-        const float e2 = (float)d.b * lx
-                       + (float)(d.b_over_r * 1.4426950408889634) * (1.0f - exp2f((float)d.r * lx));
-        return 2.0f * exp2f(e2);
+        return morse_f32(x, (float)d.b, morse_c1_f32(d), (float)d.r);
     } else if (d.kind == NW_MORLET) {
         const float x = (float)j * d.xstep32[fi];
         const float a = (float)d.sigma - x;

@@ -111,7 +111,7 @@ template <int KIND> struct RowW<float, KIND> {
     __device__ __forceinline__ void init(const WDesc& d, int fi) {
         xs = d.xstep32 ? d.xstep32[fi] : 0.0f;
         b = (float)d.b;
-        c1 = (float)(d.b_over_r * 1.4426950408889634);
+        c1 = morse_c1_f32(d);
         rr = (float)d.r;
         cpi = (float)d.cpi;
         sigma = (float)d.sigma;
@@ -134,9 +134,7 @@ template <int KIND> struct RowW<float, KIND> {
         if constexpr (KIND == NW_MORSE) {
             const float x = (float)j * xs;
             if (!(x > 0.0f)) return 0.0f;
-            const float lx = __log2f(x);
-            const float e2 = b * lx + c1 * (1.0f - exp2f(rr * lx));
-            psi = 2.0f * exp2f(e2);
+            psi = morse_f32(x, b, c1, rr);
         } else if constexpr (KIND == NW_MORLET) {
             const float x = (float)j * xs;
             const float a = sigma - x;
@@ -235,7 +233,9 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
     // bins k = k1 + n1*k2 with k2 = t + r*T: elements r >= need are zero for every thread;
     // pass 0 runs the variant NZ = nzv(need) elements
     auto need_of = [&](int k1) { return km < k1 ? 1 : (km - k1) / n1 / G::T + 1; };
-    auto nzv_of = [](int need) { return need <= 4 ? 4 : need <= 8 ? 8 : (E > 16 && need <= 16) ? 16 : E; };
+    auto nzv_of = [](int need) {
+        return need <= 4 ? 4 : need <= 8 ? 8 : (E > 16 && need <= 16) ? 16 : (E > 16 && need <= 24) ? 24 : E;
+    };
     // XD: a row whose pass 0 reads only Xt[k1][0 .. N2/2) (NZ <= E/2) gets those bins by
     // LDS-DMA into the idle image, issued BEFORE the previous row's stores (as nw_fused's
     // next-signal X): global loads issued after the stores would wait for all of them in
@@ -301,6 +301,7 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
             if (need <= 4) pass0.template operator()<4, false>();
             else if (need <= 8) pass0.template operator()<8, false>();
             else if (E > 16 && need <= 16) pass0.template operator()<(E > 16 ? 16 : E), false>();
+            else if (E > 16 && need <= 24) pass0.template operator()<(E > 16 ? 24 : E), false>();
             else pass0.template operator()<E, false>();
         }
         void* orow = B + ((int64_t)fl * n1 + k1) * N2;
@@ -318,7 +319,11 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
         }
         // B rows stored nt (fp64: the 16-B complex128 stores; plain ones made the C5 fp64 step
         // 129.4 ms against 125.3)
+#ifdef NW_B_PLAIN   // diagnostic: B with plain stores (kept in the Infinity Cache when it fits)
+        passes_from<T, N2, E, NW_OUT_CWT, 1, XD, kStoreGlobal>(v, lds, t, tw, x, xs_next, orow, nullptr, nullptr, rounds_next);
+#else
         passes_from<T, N2, E, NW_OUT_CWT, 1, XD, kStoreGlobalNt>(v, lds, t, tw, x, xs_next, orow, nullptr, nullptr, rounds_next);
+#endif
     }
 }
 
