@@ -74,6 +74,8 @@ constexpr int kWKeep32 = 16, kWKeep32Small = 8;
 // above 186 Hz), between the power-of-two variants: C4 3.360-3.368 -> 3.346-3.351 ms
 constexpr bool kNz24 = true;
 template <typename T, int N, int E> constexpr bool kNz24Of = kNz24 && E > 16;
+// NZ = 12 and 20 between them (fp32 only: fp64 n = 16384 |y| spills 20 B with them)
+template <typename T, int N, int E> constexpr bool kNzFineOf = kNz24Of<T, N, E> && sizeof(T) == 4;
 // signals per block: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (2 and 16 slower or equal).
 // fp64 (one block per CU) takes 4: an XCD round of 8 scales x 4 groups then reads W (8 x 128
 // KiB) + X (16 x 128 KiB) = 3 MiB, inside the XCD's 4 MiB L2 (8 signals: 5 MiB, re-read from
@@ -245,7 +247,9 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
         };
         if (nz <= 4) pass0.template operator()<4>();
         else if (nz <= 8) pass0.template operator()<8>();
+        else if (kNzFineOf<T, N, E> && nz <= 12) pass0.template operator()<(E > 16 ? 12 : E)>();
         else if (E > 16 && nz <= 16) pass0.template operator()<(E > 16 ? 16 : E)>();
+        else if (kNzFineOf<T, N, E> && nz <= 20) pass0.template operator()<(E > 16 ? 20 : E)>();
         else if (kNz24Of<T, N, E> && nz <= 24) pass0.template operator()<(E > 16 ? 24 : E)>();
         else pass0.template operator()<E>();
         if constexpr (XD) {
@@ -349,6 +353,9 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
         };
         if (nz <= 4) pass0.template operator()<4>();
         else if (nz <= 8) pass0.template operator()<8>();
+#ifndef NW_NO_NZ12
+        else if (nz <= 12) pass0.template operator()<12>();
+#endif
         else pass0.template operator()<E>();
         void* o1 = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;
         void* o2 = two ? (void*)((char*)out + (s2 * d.nfreq + fi) * (int64_t)N * out_esz) : nullptr;
@@ -408,9 +415,10 @@ __global__ __launch_bounds__(256) void wtable_kernel(WDesc d, void* wtab) {
 
 // Support of each W row for pass-0 pruning: wnz[f] >= the number of pass-0 elements r
 // (bins k = t + r*T, t < T) reaching the row's last nonzero bin, i.e. elements r >= wnz[f]
-// see W = 0 exactly for every thread: the next power of two up to 8, then the next multiple
-// of 8 (the pass-0 variants NZ = 4, 8, 16, 24, E; a multiple of 2^WSH, so nz >> WSH is exact
-// for the partial-sum kernels' smaller E).
+// see W = 0 exactly for every thread: the next power of two up to 4, then the next multiple
+// of 4 (the pass-0 variants: NZ = 4, 8, 12, 16 at E = 16; 4, 8, 12, 16, 20, 24, 32 at E = 32
+// fp32; a multiple of 2^WSH, so nz >> WSH is exact for the partial-sum kernels' smaller E).
+// Rows pruned in steps of 4 elements: C3 1.205 -> 1.186 ms per launch (NZ = 12 at E = 16).
 template <typename T, bool REALW>
 __global__ __launch_bounds__(256) void wsupport_kernel(const void* wtab, int64_t n, int tt, int e, int* wnz) {
     __shared__ int kmax[256];
@@ -435,7 +443,7 @@ __global__ __launch_bounds__(256) void wsupport_kernel(const void* wtab, int64_t
         const int need = kmax[0] < 0 ? 1 : kmax[0] / tt + 1;   // elements 0 .. need-1 can be nonzero
         int p2 = 1;
         while (p2 < need && p2 < 8) p2 <<= 1;
-        if (p2 < need) p2 = kNz24 ? (need + 7) / 8 * 8 : [&] { int q = 8; while (q < need) q <<= 1; return q; }();
+        if (p2 < need) p2 = (need + 3) / 4 * 4;
         wnz[fi] = p2 < e ? p2 : e;
     }
 }

@@ -233,8 +233,11 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
     // bins k = k1 + n1*k2 with k2 = t + r*T: elements r >= need are zero for every thread;
     // pass 0 runs the variant NZ = nzv(need) elements
     auto need_of = [&](int k1) { return km < k1 ? 1 : (km - k1) / n1 / G::T + 1; };
+    // pass-0 variants in steps of 4 elements at fp32 E = 32 (fp64: 4, 8, 16, 24, E)
+    constexpr bool FINE = E > 16 && sizeof(T) == 4 && KIND != NW_TABLE;   // table rows: more scratch
     auto nzv_of = [](int need) {
-        return need <= 4 ? 4 : need <= 8 ? 8 : (E > 16 && need <= 16) ? 16 : (E > 16 && need <= 24) ? 24 : E;
+        return need <= 4 ? 4 : need <= 8 ? 8 : (FINE && need <= 12) ? 12 : (E > 16 && need <= 16) ? 16
+             : (FINE && need <= 20) ? 20 : (E > 16 && need <= 24) ? 24 : E;
     };
     // XD: a row whose pass 0 reads only Xt[k1][0 .. N2/2) (NZ <= E/2) gets those bins by
     // LDS-DMA into the idle image, issued BEFORE the previous row's stores (as nw_fused's
@@ -296,11 +299,14 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
         if (XD && in_lds) {
             if (need <= 4) pass0.template operator()<4, XD>();
             else if (need <= 8) pass0.template operator()<8, XD>();
+            else if (FINE && need <= 12) pass0.template operator()<(FINE ? 12 : E), XD>();
             else pass0.template operator()<(E > 16 ? 16 : E), XD>();
         } else {
             if (need <= 4) pass0.template operator()<4, false>();
             else if (need <= 8) pass0.template operator()<8, false>();
+            else if (FINE && need <= 12) pass0.template operator()<(FINE ? 12 : E), false>();
             else if (E > 16 && need <= 16) pass0.template operator()<(E > 16 ? 16 : E), false>();
+            else if (FINE && need <= 20) pass0.template operator()<(FINE ? 20 : E), false>();
             else if (E > 16 && need <= 24) pass0.template operator()<(E > 16 ? 24 : E), false>();
             else pass0.template operator()<E, false>();
         }
