@@ -146,18 +146,29 @@ template <int KIND> struct RowW<float, KIND> {
     }
 };
 
-// fp64: psi_f64 (the reference's expression order: pow / exp on nu = j * delta, nu / f)
-// times 1/n, exactly as wavelet_bin<double>, with the per-scale loads hoisted
-// (x^b and x^r by repeated squaring instead of log / exp for small integer 2b and r measured
-// slower: its 76 B of scratch made the C5 fp64 row pass 59.7 -> 93.8 ms per step; x^3 alone,
-// round 3: 44 B of scratch, rows 0.93 -> 0.98 ms per launch)
+// fp64 rows, per-scale constants hoisted and pinned in SGPRs.  Morse in the log domain:
+// x^b e^{(b/r)(1 - x^r)} = exp(b ln x + (b/r)(1 - x^r)), x = j * (delta / f) (one multiply per
+// bin for the reference's nu / f with nu = j * delta: <= 2 ulp of x, i.e. < 1e-14 relative
+// in psi), x^r = exp(r ln x); psi(0) = 0 as np.heaviside(0, 0).  Relative error ~ |b ln x| eps
+// < 1e-13 over the rows' support.  Measured (C5 fp64 row pass): the W evaluation is 26 % of
+// it (0.937 -> 0.697 ms without it).  Morlet / Shannon: psi_f64's expression.  (x^b and x^r by
+// repeated squaring measured slower: 76 B of scratch; x^3 as x*x*x for r = 3 spills 44-64 B:
+// the exp / log polynomial constants of ocml sit in ~22 VGPRs hoisted out of the row loop.)
 template <int KIND> struct RowW<double, KIND> {
-    double delta, f, peak, b, r, bor, sigma, cpi, kappa, scale;
+    static constexpr bool MORSE = KIND == NW_MORSE;
+    double delta, f, xs, peak, b, r, bor, sigma, cpi, kappa, scale;
     int off, lenv;
+    __device__ static __forceinline__ double pin(double v) {
+        const long long u = __double_as_longlong(v);
+        const int lo = __builtin_amdgcn_readfirstlane((int)(u & 0xffffffffLL));
+        const int hi = __builtin_amdgcn_readfirstlane((int)(u >> 32));
+        return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+    }
     __device__ __forceinline__ void init(const WDesc& d, int fi) {
         delta = d.delta;
-        f = d.freq ? d.freq[fi] : 1.0;
-        peak = d.peak ? d.peak[fi] : 1.0;
+        f = pin(d.freq ? d.freq[fi] : 1.0);
+        xs = pin(delta / f);
+        peak = pin(d.peak ? d.peak[fi] : 1.0);
         b = d.b;
         r = d.r;
         bor = d.b_over_r;
@@ -170,21 +181,19 @@ template <int KIND> struct RowW<double, KIND> {
     }
     __device__ __forceinline__ double operator()(int j) const {
         if ((unsigned)j >= (unsigned)lenv) return 0.0;
-        const double nu = (double)(int64_t)j * delta;
         double psi;
-        if constexpr (KIND == NW_MORSE) {
-            // x^b e^{(b/r)(1 - x^r)} = exp(b ln x + (b/r)(1 - exp(r ln x))): one log and two
-            // exps instead of two pows (relative error ~ |b ln x| eps < 1e-13 over the rows'
-            // support; psi(0) = 0 as np.heaviside(0, 0))
-            const double x = nu / f;
+        if constexpr (MORSE) {
+            const double x = (double)j * xs;
             if (!(x > 0.0)) return 0.0;
             const double lx = log(x);
             psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
         } else if constexpr (KIND == NW_MORLET) {
+            const double nu = (double)(int64_t)j * delta;
             const double x = nu / f * peak;
             const double a = sigma - x;
             psi = cpi * (exp(-(a * a) / 2.0) - kappa * exp(-(x * x) / 2.0));
         } else {
+            const double nu = (double)(int64_t)j * delta;
             psi = nu <= 1.0 ? 1.0 : 0.0;
         }
         return psi * scale;
