@@ -318,7 +318,10 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
     const int sg = ((round / nfr) * kTileG + pos / kTileF) * 8 + xcd;
     if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
     const int64_t s_begin = (int64_t)sg * group;
-    const int64_t s_end = min(nsig, s_begin + group);
+    // the block's signal count, pinned in an SGPR: as an int64 min it sat in a VGPR pair that
+    // was spilled, and its reload at the top of every pair iteration waited (vmcnt(0)) for all
+    // of the previous pair's stores
+    const int cnt = __builtin_amdgcn_readfirstlane((int)(min(nsig, s_begin + group) - s_begin));
 
     const float* wrow = reinterpret_cast<const float*>(wtab) + (int64_t)fi * N;
     const uint32_t wo = (uint32_t)t * (uint32_t)sizeof(float);
@@ -328,7 +331,7 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
     Tab1<f2, N, E>::fill(lds, tw, t);
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<float>) : sizeof(float));
     const int nz = wnz[fi];
-    NW_DCHECK(fi < d.nfreq && s_end <= nsig && d.n == N && nz >= 1 && nz <= E);
+    NW_DCHECK(fi < d.nfreq && s_begin + cnt <= nsig && d.n == N && nz >= 1 && nz <= E);
     auto xrow = [&](int64_t s) { return reinterpret_cast<const C2<float>*>(X + s * d.nh); };
     // power partial sums (kOutPSum): as nw_fused_kernel, both signals of a pair into one sum
     constexpr bool PSUM = OUT == kOutPSum;
@@ -337,8 +340,9 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
 #pragma unroll
         for (int e = 0; e < E; ++e) acc[e] = 0.0;
     }
-    for (int64_t s = s_begin; s < s_end; s += 2) {
-        const bool two = s + 1 < s_end;
+    for (int i = 0; i < cnt; i += 2) {
+        const int64_t s = s_begin + i;
+        const bool two = i + 1 < cnt;
         const int64_t s2 = two ? s + 1 : s;
         C2<f2> v[E];
         auto pass0 = [&]<int NZ>() {
