@@ -525,13 +525,33 @@ __device__ __forceinline__ void dma_x(const C2<T>* xs, void* dst, int t, int nro
 #pragma unroll
     for (int i = 0; i < CH / TT; ++i) {
         if (i >= nround) break;
-        // uniform chunk base + opaque 32-bit lane offset: the saddr form, no 64-bit VGPR pairs
+        // uniform chunk base + 32-bit lane offset: the saddr form, no 64-bit VGPR pairs
         const char* chunk = reinterpret_cast<const char*>(xs) + (size_t)i * TT * 16;
         asm volatile("" : "+s"(chunk));           // computed here, in SGPRs (not hoisted)
-        const char* src = at(chunk, lane_off);
-        __builtin_amdgcn_global_load_lds((gbl_void_t*)src,
-                                         (lds_void_t*)(reinterpret_cast<char*>(dst) + i * TT * 16 + wave_base), 16,
-                                         0, 0);
+        const uint32_t lds_addr = (uint32_t)(uintptr_t)(lds_void_t*)(reinterpret_cast<char*>(dst) + i * TT * 16 + wave_base);
+        // Issued as inline asm, not __builtin_amdgcn_global_load_lds: for the builtin the
+        // compiler puts a vmcnt(0) before every later LDS read (it cannot count a loop-carried,
+        // variably sized DMA), which also waits for all of the previous signal's stores.  The
+        // callers order it themselves: a barrier before (the image's readers are done) and
+        // wait_vmcnt<#stores issued after it> + a barrier before the first read.
+        asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2"
+                     :: "s"(lds_addr), "v"(lane_off), "s"(chunk) : "memory", "m0");
+    }
+}
+
+// One uniform complex value by a scalar load (lgkmcnt, not vmcnt): a vector load issued
+// after the previous signal's stores would wait for all of them (in-order vmcnt), and the
+// compiler put a vmcnt(0) before it (a register of the merged pass-0 variants still pending)
+template <typename T> __device__ __forceinline__ C2<T> sload_c2(const C2<T>* p) {
+    if constexpr (sizeof(T) == 4) {
+        unsigned long long u;
+        asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(u) : "s"(p) : "memory");
+        return C2<T>{__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32))};
+    } else {
+        typedef unsigned long long u2 __attribute__((ext_vector_type(2)));
+        u2 u;
+        asm volatile("s_load_dwordx4 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(u) : "s"(p) : "memory");
+        return C2<T>{__longlong_as_double((long long)u.x), __longlong_as_double((long long)u.y)};
     }
 }
 

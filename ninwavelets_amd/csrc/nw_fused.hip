@@ -253,7 +253,7 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
         else if (kNz24Of<T, N, E> && nz <= 24) pass0.template operator()<(E > 16 ? 24 : E)>();
         else pass0.template operator()<E>();
         if constexpr (XD) {
-            if (s + 1 < s_end) nyq = reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh)[N / 2];
+            if (s + 1 < s_end) nyq = sload_c2(reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) + N / 2);
         }
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
