@@ -542,6 +542,16 @@ __device__ __forceinline__ void dma_x(const C2<T>* xs, void* dst, int t, int nro
 // One uniform complex value by a scalar load (lgkmcnt, not vmcnt): a vector load issued
 // after the previous signal's stores would wait for all of them (in-order vmcnt), and the
 // compiler put a vmcnt(0) before it (a register of the merged pass-0 variants still pending)
+// fp32: the raw 8 bytes (kept uniform, in SGPRs, across a loop; C2 values of it were moved
+// to VGPRs and spilled to scratch, whose reload is a vector load behind the stores)
+__device__ __forceinline__ unsigned long long sload_u64(const void* p) {
+    unsigned long long u;
+    asm volatile("s_load_dwordx2 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=s"(u) : "s"(p) : "memory");
+    return u;
+}
+__device__ __forceinline__ C2<float> c2_of_u64(unsigned long long u) {
+    return C2<float>{__uint_as_float((unsigned)u), __uint_as_float((unsigned)(u >> 32))};
+}
 template <typename T> __device__ __forceinline__ C2<T> sload_c2(const C2<T>* p) {
     if constexpr (sizeof(T) == 4) {
         unsigned long long u;
@@ -716,7 +726,7 @@ template <typename T, int N, int E, int OUT, int P, bool XD, int SP = kStoreGlob
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
                                             Stamps* st, void* ocur2 = nullptr, int dma_rounds = 1 << 30,
-                                            double* acc = nullptr) {
+                                            double* acc = nullptr, const void* xs_next2 = nullptr) {
     using S = Sc<T>;
     constexpr bool PAIRSIG = !std::is_same<T, S>::value;
     constexpr int OSZ = (int)sizeof(typename OutT<OUT, S>::type);
@@ -756,8 +766,14 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
         if constexpr (I::LAST && XD) {
             if (xs_next) {                     // the image is idle once every wave has read it
                 lds_barrier();
-                static_assert(!PAIRSIG, "the signal-pair kernel reads X from L2");
-                dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t, dma_rounds);
+                if constexpr (PAIRSIG) {
+                    // the next pair's two half spectra side by side: [0, N/2) and [N/2, N) complex
+                    dma_x<S, N, Geometry<N, E>::T>(reinterpret_cast<const C2<S>*>(xs_next), lds, t, dma_rounds);
+                    dma_x<S, N, Geometry<N, E>::T>(reinterpret_cast<const C2<S>*>(xs_next2),
+                                                   reinterpret_cast<char*>(lds) + (N / 2) * sizeof(C2<S>), t, dma_rounds);
+                } else {
+                    dma_x<T, N, Geometry<N, E>::T>(xs_next, lds, t, dma_rounds);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -879,7 +895,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                 LastStores<T, N, E, OUT, SP>::all(v, ocur, t);
             }
         } else {
-            passes_from<T, N, E, OUT, P + 1, XD, SP>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, acc);
+            passes_from<T, N, E, OUT, P + 1, XD, SP>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, acc, xs_next2);
         }
     }
 }

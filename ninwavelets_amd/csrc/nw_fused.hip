@@ -73,6 +73,11 @@ constexpr int kWKeep32 = 16, kWKeep32Small = 8;
 // E = 32: a pass-0 variant for rows whose support ends below 3/4 of n (NZ = 24: C4's rows
 // above 186 Hz), between the power-of-two variants: C4 3.360-3.368 -> 3.346-3.351 ms
 constexpr bool kNz24 = true;
+// signal-pair kernel: the next pair's X by LDS-DMA before the stores
+#ifndef NW_PAIR_XD
+#define NW_PAIR_XD 1
+#endif
+constexpr bool kPairXD = NW_PAIR_XD;
 template <typename T, int N, int E> constexpr bool kNz24Of = kNz24 && E > 16;
 // NZ = 12 and 20 between them (fp32 only: fp64 n = 16384 |y| spills 20 B with them)
 template <typename T, int N, int E> constexpr bool kNzFineOf = kNz24Of<T, N, E> && sizeof(T) == 4;
@@ -294,9 +299,8 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
 // (v_pk_add/mul/fma_f32; 8-B image slots; twiddles and the pass-1 table shared).  Pass 0
 // reads both X rows and the block's W registers; the last pass stores each half to its
 // own row (an odd last signal transforms a duplicate whose high half is not stored).
-// X is read from L2 in pass 0 (the next pair's X by LDS-DMA measured slower: C3 1.257 ->
-// 1.356 ms, n = 1024 / 2048 +4 %, as the single-signal E = 16 DMA).  4 waves/SIMD; the power
-// partials' E fp64 accumulators take it to 3.
+// |y| and |y|^2 read X from L2 in pass 0; cwt takes the next pair's X by LDS-DMA before the
+// stores (XD below).  4 waves/SIMD; the power partials' E fp64 accumulators take it to 3.
 template <int N, int E, int OUT>
 __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_kernel(WDesc d, const cplx<float>* __restrict__ X,
                                                                   const void* __restrict__ wtab, void* __restrict__ out,
@@ -333,6 +337,22 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
     const int nz = wnz[fi];
     NW_DCHECK(fi < d.nfreq && s_begin + cnt <= nsig && d.n == N && nz >= 1 && nz <= E);
     auto xrow = [&](int64_t s) { return reinterpret_cast<const C2<float>*>(X + s * d.nh); };
+    // XD: the next pair's X[0 .. N/2) (both signals, or only the bins a pruned pass 0 reads) by
+    // LDS-DMA into the idle image before the stores, as nw_fused_kernel at E = 32; the Nyquist
+    // bins by scalar loads
+    // (cwt only: n = 4096 cwt 1.585 -> 1.567 ms per 256-signal launch; |y|^2 slower, C3 1.180 ->
+    // 1.210, n = 1024 power equal)
+    constexpr bool XD = kPairXD && OUT == NW_OUT_CWT;
+    const int nzv = nz < kPruneMin ? kPruneMin : nz;
+    const int dma_rounds = nzv <= E / 2 ? dma_rounds_for<float>(nzv) : 1 << 30;
+    unsigned long long nyq_a = 0, nyq_b = 0;
+    if constexpr (XD) {
+        const int64_t sb = cnt > 1 ? s_begin + 1 : s_begin;
+        nyq_a = sload_u64(xrow(s_begin) + N / 2);
+        nyq_b = sload_u64(xrow(sb) + N / 2);
+        dma_x<float, N, G::T>(xrow(s_begin), lds, t, dma_rounds);
+        dma_x<float, N, G::T>(xrow(sb), reinterpret_cast<char*>(lds) + (N / 2) * sizeof(C2<float>), t, dma_rounds);
+    }
     // power partial sums (kOutPSum): as nw_fused_kernel, both signals of a pair into one sum
     constexpr bool PSUM = OUT == kOutPSum;
     double acc[PSUM ? E : 1];
@@ -345,10 +365,45 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
         const bool two = i + 1 < cnt;
         const int64_t s2 = two ? s + 1 : s;
         C2<f2> v[E];
+        if constexpr (XD) {
+            // this wave's DMA landed (only the previous pair's 2 x COUNT stores may be pending),
+            // then every wave's
+            if (i == 0) wait_vmcnt<0>(); else wait_vmcnt<2 * LastStores<float, N, E, OUT, kStoreBuffer>::COUNT>();
+            lds_barrier();
+        }
         auto pass0 = [&]<int NZ>() {
             C2<float> xa[E], xb[E];
-            load_x<float, N, E, NZ>(xa, xrow(s), t);
-            load_x<float, N, E, NZ>(xb, xrow(s2), t);
+            if constexpr (XD) {
+                int tl = t;                         // opaque: the LDS reads stay below the dispatch
+                asm volatile("" : "+v"(tl));
+                const C2<float>* la = reinterpret_cast<const C2<float>*>(lds);
+                const C2<float>* lb = la + N / 2;
+                const C2<float>* ma = la + (N - (E - 1) * G::T - tl);
+                const C2<float>* mb = lb + (N - (E - 1) * G::T - tl);
+#pragma unroll
+                for (int r = 0; r < NZ; ++r) {
+                    if (r < E / 2) {
+                        xa[r] = la[tl + r * G::T];
+                        xb[r] = lb[tl + r * G::T];
+                    } else {                        // X[N - k]; k = N/2 (t = 0, r = E/2) is the Nyquist bin
+                        C2<float> va = ma[(E - 1 - r) * G::T], vb = mb[(E - 1 - r) * G::T];
+                        if (r == E / 2) {
+                            // values in registers first: a select of the two sources would become
+                            // a load through a selected pointer (the Nyquist bin via scratch)
+                            asm volatile("" : "+v"(va.re), "+v"(va.im), "+v"(vb.re), "+v"(vb.im));
+                            const C2<float> na = c2_of_u64(nyq_a), nb = c2_of_u64(nyq_b);
+                            const bool z = t == 0;
+                            va = C2<float>{z ? na.re : va.re, z ? na.im : va.im};
+                            vb = C2<float>{z ? nb.re : vb.re, z ? nb.im : vb.im};
+                        }
+                        xa[r] = C2<float>{va.re, -va.im};
+                        xb[r] = C2<float>{vb.re, -vb.im};
+                    }
+                }
+            } else {
+                load_x<float, N, E, NZ>(xa, xrow(s), t);
+                load_x<float, N, E, NZ>(xb, xrow(s2), t);
+            }
 #pragma unroll
             for (int r = 0; r < E; ++r)
                 v[r] = r < NZ ? C2<f2>{f2{w[r] * xa[r].re, w[r] * xb[r].re}, f2{w[r] * xa[r].im, w[r] * xb[r].im}}
@@ -363,8 +418,20 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
         else pass0.template operator()<E>();
         void* o1 = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;
         void* o2 = two ? (void*)((char*)out + (s2 * d.nfreq + fi) * (int64_t)N * out_esz) : nullptr;
-        passes_from<f2, N, E, OUT, 1, false, kStoreBuffer>(v, lds, t, tw, nullptr, nullptr, o1, nullptr, o2, 1 << 30,
-                                             PSUM ? acc : nullptr);
+        // the next pair (signals s + 2 and s + 3, or s + 2 twice when it is the odd last one)
+        const C2<float>* xn_a = nullptr;
+        const C2<float>* xn_b = nullptr;
+        if constexpr (XD) {
+            if (i + 2 < cnt) {
+                xn_a = xrow(s + 2);
+                xn_b = i + 3 < cnt ? xrow(s + 3) : xn_a;
+                nyq_a = sload_u64(xn_a + N / 2);
+                nyq_b = sload_u64(xn_b + N / 2);
+            }
+        }
+        passes_from<f2, N, E, OUT, 1, XD, kStoreBuffer>(v, lds, t, tw, nullptr,
+                                                       reinterpret_cast<const C2<f2>*>(xn_a), o1, nullptr, o2,
+                                                       dma_rounds, PSUM ? acc : nullptr, xn_b);
     }
     if constexpr (PSUM) {
         using IL = PassInfo<N, E, G::npass() - 1, (int)sizeof(float), true>;
