@@ -48,7 +48,7 @@ CONFIGS = {
            'C2 Morlet CWT, 64 ch x 16384 samples x 128 freqs per GPU, complex64 out'),
     'c5': ('morse', 1, 1, 1 << 24, np.linspace(0.5, 250, 512), 'cwt', 'float32',
            'C5 Morse CWT, 1 signal x 2^24 samples x 512 freqs (linspace 0.5..250) per GPU, '
-           'complex64 out (68.7 GB, written into one HBM buffer)'),
+           'complex64 out (written into one HBM buffer)'),
 }
 
 
@@ -260,23 +260,26 @@ def fft_flops_per_row(n: int, kname: str) -> float:
     return 5.0 * n * math.log2(n) + 2.0 * n
 
 
-def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg, dtype_override=None, fp64_leg=False):
+def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name, dtype_override=None, fp64_leg=False,
+            overrides=True):
     """One measured workload: warmup, barrier-bracketed timed steps, max over ranks.
-    Returns (line fields, plan stats, extra) for rank 0's JSON line."""
-    kind, epochs, chans, n, freqs, out_kind, dtype, text = cfg
-    if args.epochs:
+    Returns (line fields, plan stats, extra) for rank 0's JSON line.  overrides=False: the
+    config as CONFIGS names it (the extra legs of the default line ignore the diagnostic
+    flags; --epochs still scales the multi-epoch legs down, for tests)."""
+    kind, epochs, chans, n, freqs, out_kind, dtype, text = CONFIGS[cfg_name]
+    if args.epochs and (overrides or epochs > 1):
         epochs = args.epochs
-    if args.output:
+    if overrides and args.output:
         out_kind = args.output
-    if args.samples:
+    if overrides and args.samples:
         n = args.samples
-    if args.wavelet and args.wavelet != kind:
+    if overrides and args.wavelet and args.wavelet != kind:
         text = text.replace(kind.capitalize(), args.wavelet.capitalize(), 1)
         kind = args.wavelet
         if kind == 'shannon':
             text += (' [Shannon ignores the freq (wavelets.py:256-262): its one distinct row is '
                      'computed once per signal and copied to every scale]')
-    want = dtype_override or args.dtype
+    want = dtype_override or (args.dtype if overrides else None)
     if want and want != dtype:
         dtype = want
         text = (text.replace('complex64 out', 'complex128 out') if fp64_leg else
@@ -289,7 +292,7 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg, dtype_over
         f0, f1 = shard(F, rank, world)
         freqs = freqs[f0:f1]
         F = f1 - f0
-    C = min(args.chunk or DEFAULT_CHUNK.get(args.config, 256), S)
+    C = min((args.chunk if overrides else None) or DEFAULT_CHUNK.get(cfg_name, 256), S)
     f64 = dtype == 'float64'
     x = synth_device(torch, S, n, seed=1000 + (0 if by_scales else rank), device=dev,
                      dtype=torch.float64 if f64 else torch.float32)
@@ -315,7 +318,7 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg, dtype_over
         if world > 1:
             dist.barrier()
 
-    log(f'[bench] rank {rank}/{world} {args.config}{" fp64 leg" if fp64_leg else ""}: S={S} n={n} F={F} '
+    log(f'[bench] rank {rank}/{world} {cfg_name}{" fp64 leg" if fp64_leg else ""}: S={S} n={n} F={F} '
         f'chunk={C} dtype={dtype} engine={plan.stats()["engine"]} device={dev}')
     for w in range(args.warmup):
         step()
@@ -335,14 +338,14 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg, dtype_over
            'workload': text, 'kind': kind, 'epochs': epochs * (1 if by_scales else world), 'chans': chans,
            'n': n, 'freqs': freqs, 'F': F, 'F_all': F_all, 'out_kind': out_kind, 'chunk': C,
            'by_scales': by_scales, 'dtype_name': dtype}
-    extra = roofline_of(args, st, S, F, n, C, out_kind, dtype, esz, el, L) if rank == 0 else {}
+    extra = roofline_of(args, cfg_name, st, S, F, n, C, out_kind, dtype, esz, el, L) if rank == 0 else {}
     plan.close()
     del bufs, x
     torch.cuda.empty_cache()
     return res, st, extra
 
 
-def roofline_of(args, st, S, F, n, C, out_kind, dtype, esz, el, L):
+def roofline_of(args, cfg_name, st, S, F, n, C, out_kind, dtype, esz, el, L):
     """The dominant kernel's HBM roofline (event-timed average launch, algorithmic bytes),
     its VALU roofline (nominal FFT flops) and the end-to-end figures."""
     f64 = dtype == 'float64'
@@ -389,6 +392,10 @@ def roofline_of(args, st, S, F, n, C, out_kind, dtype, esz, el, L):
             'achieved': round(rows_bytes / (rows_ms * 1e-3) / 1e9, 1), 'peak': PEAK_HBM_GBPS,
             'unit': 'GB/s', 'frac': round(rows_bytes / (rows_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS, 4),
             'avg_launch_ms': round(rows_ms, 4), 'algorithmic_bytes_per_launch': rows_bytes}
+        rt, rsrc = pmc_traffic('rows_kernel', cfg_name, C, st['engine'], dtype, out_kind, n)
+        extra['roofline_rows'].update(traffic=rt, traffic_source=(
+            f'{rsrc}: rocprofv3 PMC passes, 2*FETCH_SIZE + WRITE_SIZE per launch, on engine sources '
+            f'{source_hash()}' if rsrc else 'no PMC summary on the current engine sources'))
     else:
         per_launch = C * ((n // 2 + 1) * 2 * esz + F * n * out_e)   # X read once + out written once
         kname = L.KERNEL_NAMES[st['kernel']]          # the kernel rocprofv3 shows for this launch
@@ -401,7 +408,7 @@ def roofline_of(args, st, S, F, n, C, out_kind, dtype, esz, el, L):
             'achieved': round(min_bytes / (el / args.steps) / 1e9, 1), 'unit': 'GB/s',
             'frac': round(min_bytes / (el / args.steps) / 1e9 / PEAK_HBM_GBPS, 4)}
     achieved = per_launch / (ms * 1e-3) / 1e9
-    traffic, traffic_src = pmc_traffic(kname, args.config, C, st['engine'], dtype, out_kind, n)
+    traffic, traffic_src = pmc_traffic(kname, cfg_name, C, st['engine'], dtype, out_kind, n)
     roof = {'kernel': kname, 'bound': 'hbm',
             'achieved': round(achieved, 1), 'peak': PEAK_HBM_GBPS, 'unit': 'GB/s',
             'frac': round(achieved / PEAK_HBM_GBPS, 4),
@@ -432,6 +439,23 @@ def roofline_of(args, st, S, F, n, C, out_kind, dtype, esz, el, L):
     return extra
 
 
+# extra legs of the default line: key -> (config, compute dtype)
+LEGS = {'fp64': ('c4', 'float64'), 'c3': ('c3', 'float32'), 'c5': ('c5', 'float32'), 'c5_fp64': ('c5', 'float64')}
+
+
+def leg_fields(r, st, ex):
+    """One extra leg's fields on the default line: its value, its workload, the dominant
+    kernel's HBM roofline (+ the row pass's for the two-pass form), the VALU roofline and
+    the end-to-end figure against the path's minimum traffic."""
+    d = {'value': r['value'], 'unit': 'points/s', 'ms_per_step': r['ms_per_step'], 'dtype': r['dtype'],
+         'workload': r['workload'], 'output': r['out_kind'], 'chunk_signals': r['chunk'], 'engine': st['engine'],
+         'roofline': ex['roofline']}
+    for k in ('roofline_rows', 'valu_roofline', 'end_to_end_min_traffic', 'computed_rows', 'stage_ms_per_step'):
+        if k in ex:
+            d[k] = ex[k]
+    return d
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -459,6 +483,9 @@ def main(argv=None):
     ap.add_argument('--no-fp64', action='store_true',
                     help='skip the fp64 leg (the same workload at the reference\'s complex128 precision, '
                          'reported under the "fp64" key of the default C4 line)')
+    ap.add_argument('--legs', default=','.join(LEGS),
+                    help='extra legs of the default C4 line, comma-separated (default: all of '
+                         f'{",".join(LEGS)}; "none" for none)')
     ap.add_argument('--backend', default=None, choices=['nccl', 'gloo'],
                     help='process-group backend for N > 1 ranks (default: nccl = RCCL over xGMI; '
                          'gloo with --dry-run)')
@@ -470,6 +497,9 @@ def main(argv=None):
                          'barriers and the max-over-ranks timing on CPU (tests)')
     ap.add_argument('--fail-rank', type=int, default=None, help=argparse.SUPPRESS)   # tests: that rank exits 3
     args = ap.parse_args(argv)
+    bad = [l for l in args.legs.split(',') if l and l != 'none' and l not in LEGS]
+    if bad:
+        raise SystemExit(f'bench.py: unknown --legs {bad} (choose from {sorted(LEGS)})')
 
     if 'WORLD_SIZE' in os.environ:           # torchrun or our own launcher: this process is a rank
         world = int(os.environ['WORLD_SIZE'])
@@ -506,20 +536,26 @@ def main(argv=None):
     dev = torch.device('cuda', local)
     torch.cuda.set_device(dev)
 
-    res, st, extra = run_leg(args, torch, dist, nw, L, world, rank, dev, backend, CONFIGS[args.config])
-    # the reference's own precision (complex128, base.py:399-406): the default C4 line also
-    # carries the same workload computed in fp64, with its own roofline
-    fp64 = None
-    want_fp64 = (args.config == 'c4' and res['dtype'] == 'f32' and not args.no_fp64 and not args.dtype and
-                 not args.output and not args.samples and not args.wavelet)
-    if want_fp64:
-        r64, st64, ex64 = run_leg(args, torch, dist, nw, L, world, rank, dev, backend, CONFIGS[args.config],
-                                  dtype_override='float64', fp64_leg=True)
+    res, st, extra = run_leg(args, torch, dist, nw, L, world, rank, dev, backend, args.config)
+    # The default (C4) line also carries BASELINE.json's other headline workloads, each measured
+    # in this same run after the previous leg's buffers are freed, with its own roofline:
+    #   fp64: C4 at the reference's precision (complex128 out, base.py:399-406);
+    #   c3:   Morse power 512 x 64 x 4096 x 256 (the fused |.|^2 path, base.py:409-425);
+    #   c5:   Morse cwt 1 x 2^24 x 512, fp32 and fp64 (the long-signal regime, base.py:404-406).
+    default_line = (args.config == 'c4' and res['dtype'] == 'f32' and not args.dtype and not args.output and
+                    not args.samples and not args.wavelet and not args.chunk)
+    want = [l for l in args.legs.split(',') if l and l != 'none']
+    legs = [] if not default_line else [l for l in LEGS if l in want and not (args.no_fp64 and l == 'fp64')]
+    leg_out = {}
+    for leg in legs:
+        cfg_name, dt = LEGS[leg]
+        r_, st_, ex_ = run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name,
+                               dtype_override=dt, fp64_leg=(dt == 'float64'), overrides=(leg == 'fp64'))
         if rank == 0:
-            fp64 = {'value': r64['value'], 'unit': 'points/s', 'ms_per_step': r64['ms_per_step'], 'dtype': 'f64',
-                    'workload': r64['workload'], 'chunk_signals': r64['chunk'], 'engine': st64['engine'],
-                    'roofline': ex64['roofline'], 'valu_roofline': ex64.get('valu_roofline'),
-                    'stage_ms_per_step': ex64['stage_ms_per_step']}
+            leg_out[leg] = leg_fields(r_, st_, ex_)
+    fp64 = leg_out.pop('fp64', None)
+    if 'c5' in leg_out or 'c5_fp64' in leg_out:
+        leg_out['c5'] = {'fp32': leg_out.pop('c5', None), 'fp64': leg_out.pop('c5_fp64', None)}
 
     if rank == 0:
         cpu = cpu_pool = None
@@ -546,7 +582,7 @@ def main(argv=None):
                                        f'no collective)' if res['by_scales'] else
                                        f'dp{world} (signals sharded, no collective)'),
                        **({'backend': backend, 'same_device': True} if args.same_device else {})},
-            'roofline': roof, **extra, 'fp64': fp64, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool,
+            'roofline': roof, **extra, 'fp64': fp64, **leg_out, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool,
             'stage_ms_per_step': stage_ms,
         }
         print(json.dumps(line), flush=True)

@@ -120,6 +120,10 @@ typedef struct nw_stats {
     int64_t launches_expand;
     int64_t unique_rows;    /* scale rows actually computed (nfreq unless rows repeat) */
     int64_t kernel;         /* NW_K_*: the output-writing kernel of the last chunk */
+    int64_t device_bytes;   /* device memory the plan holds now: input / spectrum / output /
+                               reduction buffers, wavelet tables, two-pass scratch, rocFFT work
+                               (it grows as calls need larger buffers; the Python classes
+                               bound their plan cache by it) */
 } nw_stats;
 
 /* nw_stats.kernel: which kernel wrote the output rows (the dominant kernel of a step) */

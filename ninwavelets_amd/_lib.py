@@ -57,7 +57,7 @@ class nw_stats(ctypes.Structure):
                 ('engine', ctypes.c_int64), ('ms_rows', ctypes.c_double),
                 ('launches_rows', ctypes.c_int64), ('ms_expand', ctypes.c_double),
                 ('launches_expand', ctypes.c_int64), ('unique_rows', ctypes.c_int64),
-                ('kernel', ctypes.c_int64)]
+                ('kernel', ctypes.c_int64), ('device_bytes', ctypes.c_int64)]
 
     def as_dict(self):
         return {name: getattr(self, name) for name, _ in self._fields_}

@@ -18,6 +18,7 @@ in libninwave.so; there is no CPU compute path.
 from __future__ import annotations
 
 import os
+from collections import OrderedDict
 from enum import Enum
 from functools import partial
 
@@ -30,6 +31,11 @@ from .engine import make_wavelets as _make_wavelets_dev
 
 # Device working-set budget per plan chunk (bytes); signals are streamed through it.
 CHUNK_BYTES = int(os.environ.get('NINWAVE_CHUNK_BYTES', str(4 << 30)))
+# Device bytes the plans cached by one wavelet object may hold together (nw_stats.device_bytes).
+# Plans are keyed on (n, batch, device, ...): a session whose epoch lengths or batch sizes vary
+# creates a plan per combination, so the least recently used ones are destroyed (their buffers
+# freed) once the total exceeds this; the plans of the current call are always kept.
+PLAN_CACHE_BYTES = int(os.environ.get('NINWAVE_PLAN_CACHE_BYTES', str(16 << 30)))
 
 
 class WaveletMode(Enum):
@@ -97,7 +103,8 @@ class WaveletBase:
         self.engine = engine
         self._cache: _Cache | None = None
         self._rows = None
-        self._plans: dict = {}
+        self._plans: OrderedDict = OrderedDict()     # least recently used first
+        self.plan_cache_bytes = PLAN_CACHE_BYTES
 
     # ------------------------------------------------------------------ plugin API
     def peak_freq(self, freq: float) -> float:
@@ -295,6 +302,7 @@ class WaveletBase:
         if plan is None:
             plan = Plan(n, nf, self.dtype, device, batch, self.interpolate, self.engine)
             self._plans[key] = plan
+        self._plans.move_to_end(key)
         if plan.wavelet_token != c.version:
             sl = slice(f0, f1)
             plan.set_wavelet(c.kind, c.params, c.freqs[sl], c.grid,
@@ -302,9 +310,33 @@ class WaveletBase:
                              row_len=None if c.row_len is None else c.row_len[sl])
         return plan
 
+    def plan_cache_device_bytes(self) -> int:
+        """Device bytes held by the cached plans (sum of nw_stats.device_bytes)."""
+        return sum(p.stats()['device_bytes'] for p in self._plans.values())
+
+    def _evict_plans(self, keep: int) -> None:
+        """Destroy least-recently-used plans (freeing their device buffers) while the cache
+        holds more than ``plan_cache_bytes``; the ``keep`` most recent (this call's) stay."""
+        sizes = {k: p.stats()['device_bytes'] for k, p in self._plans.items()}
+        total = sum(sizes.values())
+        while total > self.plan_cache_bytes and len(self._plans) > keep:
+            k, p = self._plans.popitem(last=False)
+            total -= sizes[k]
+            p.close()
+
     def _run(self, x: np.ndarray, out_kind: str) -> np.ndarray:
-        """x: (..., n) signals -> (..., F, n) on the device(s).  Several devices shard the
-        signals, or -- with fewer signals than devices (one long signal) -- the scales."""
+        """x: (..., n) signals -> (..., F, n) on the device(s); the plan cache is trimmed
+        to ``plan_cache_bytes`` after the call (its buffers grow during the call)."""
+        self._used = 1
+        try:
+            return self._run_plans(x, out_kind)
+        finally:
+            if len(self._plans) > 1:
+                self._evict_plans(keep=max(1, self._used))
+
+    def _run_plans(self, x: np.ndarray, out_kind: str) -> np.ndarray:
+        """Several devices shard the signals, or -- with fewer signals than devices (one
+        long signal) -- the scales."""
         n = x.shape[-1]
         nsig = int(np.prod(x.shape[:-1])) if x.ndim > 1 else 1
         devs = self.devices or [self.device]
@@ -312,6 +344,7 @@ class WaveletBase:
         if len(devs) > 1 and nsig < len(devs) and nf >= len(devs):
             from .dist import shard
             plans = [self._plan(n, nsig, d, shard(nf, i, len(devs)), slot=i) for i, d in enumerate(devs)]
+            self._used = len(plans)
             out = execute_multi(plans, x.reshape(nsig, n), out_kind, shard='scales')
             if out_kind in REDUCTIONS:
                 return out
@@ -319,10 +352,12 @@ class WaveletBase:
         if len(devs) > 1 and nsig > 1:
             per = -(-nsig // len(devs))          # the largest balanced block (dist.shard)
             plans = [self._plan(n, per, d, slot=i) for i, d in enumerate(devs)]
+            self._used = len(plans)
             out = execute_multi(plans, x.reshape(nsig, n), out_kind)
             if out_kind in REDUCTIONS:
                 return out
             return out.reshape(x.shape[:-1] + out.shape[-2:])
+        self._used = 1
         return self._plan(n, nsig, devs[0]).execute(x, out_kind=out_kind)
 
     def _broadcast_quirk(self, wave: np.ndarray, out_kind: str) -> np.ndarray:

@@ -171,6 +171,7 @@ struct nw_plan {
     double* d_peak = nullptr;
     float* d_xstep32 = nullptr;
     void* d_table = nullptr;
+    size_t d_table_bytes = 0;
     int64_t* d_row_len = nullptr;
     std::vector<int64_t> row_len_host;   // tables: true length of each row
 
@@ -681,8 +682,10 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     // the partials of the distinct rows are expanded like any output row)
     // The chirp-z form (lengths 2n - 1 <= M_max, every row on chip) read-modify-writes its
     // block partial rows instead (no accumulator registers; any kind, fp32 and fp64); its
-    // tentative lengths (rows may leave the chip) and the repeated-row view keep the chunk path
-    bool chirp_psum = fused && p->chirp && !p->chirp_tentative && !p->dedup;
+    // tentative lengths (rows may leave the chip) and the repeated-row view keep the chunk path;
+    // so do complex table rows (MexicanHat, Haar, user tables), as on the fused form: their
+    // partial-sum instantiations are not scratch-free (fp32 M = 4096: 20 B)
+    bool chirp_psum = fused && p->chirp && !p->chirp_tentative && !p->dedup && p->desc.kind != NW_TABLE;
     if (chirp_psum) {
         NW_TRY(chirp_table(p));   // the rows' M classes decide (chirp_psum_ok)
         chirp_psum = p->chirp && p->chirp_over.empty() && nw::chirp_psum_ok(p->dtype, phase, p->chirp_counts);
@@ -959,6 +962,7 @@ static int build_normal_table(nw_plan* p, int kind, const double* params, int np
     if (hip(hipMalloc(&d_rows, F * sizeof(nw::NormalRow)), "hipMalloc") &&
         hip(hipMalloc(&d_buf, (size_t)std::max<int64_t>(off, 1) * 2 * sizeof(double)), "hipMalloc") &&
         hip(hipMalloc(&p->d_table, std::max<size_t>(tbytes, 16)), "hipMalloc") &&
+        ((p->d_table_bytes = std::max<size_t>(tbytes, 16)), true) &&
         hip(hipMalloc((void**)&p->d_row_len, F * sizeof(int64_t)), "hipMalloc") &&
         hip(hipMemcpy(d_rows, rows.data(), F * sizeof(nw::NormalRow), hipMemcpyHostToDevice), "H2D") &&
         hip(hipMemcpy(p->d_row_len, lens.data(), F * sizeof(int64_t), hipMemcpyHostToDevice), "H2D") &&
@@ -1122,6 +1126,7 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
     if (p->d_table) {
         NW_HIP(hipFree(p->d_table));
         p->d_table = nullptr;
+        p->d_table_bytes = 0;
     }
     if (p->d_row_len) {
         NW_HIP(hipFree(p->d_row_len));
@@ -1151,6 +1156,7 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
         const size_t cnt = (size_t)F * grid->len_full;
         const size_t bytes = cnt * 2 * p->esz;
         NW_HIP(hipMalloc(&p->d_table, bytes));
+        p->d_table_bytes = bytes;
         if (p->dtype == NW_F64) {
             NW_HIP(hipMemcpy(p->d_table, table, bytes, hipMemcpyHostToDevice));
         } else {
@@ -1247,6 +1253,9 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     if (host && p->engine == NW_ENGINE_FUSED) NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * row_out));
     if (host && p->engine == NW_ENGINE_ROCFFT && out_kind == NW_OUT_CWT) NW_TRY(need_Y(p));
     // (rocFFT engine, host CWT: the complex result is read back straight from d_Y)
+    // a fresh host array (the reference returns a new one per call) is populated in parallel
+    // first, on huge pages where the kernel grants them, instead of page by page in the copy
+    if (host) nw::host::prefault_output((char*)out, (size_t)nsig * row_out, kCopyThreads);
 
     for (int64_t s0 = 0; s0 < nsig; s0 += p->max_batch) {
         const int64_t c = std::min<int64_t>(p->max_batch, nsig - s0);
@@ -1689,6 +1698,11 @@ int nw_plan_stats(nw_plan* p, nw_stats* s) {
     DeviceGuard guard(p->device);
     NW_TRY(resolve_timing(p));
     *s = p->stats;
+    // the sized buffers (the per-freq arrays, row maps and rocFFT plan objects are small)
+    s->device_bytes = (int64_t)((size_t)p->max_batch * p->n * p->esz + (size_t)p->max_batch * p->nh * 2 * p->esz +
+                                p->d_table_bytes + p->d_uout_bytes + p->d_Y_bytes + p->d_out_bytes + p->d_acc_bytes +
+                                p->d_part_bytes + p->d_gather_bytes + p->d_wtab_bytes + p->d_oscr_bytes +
+                                p->d_scratch_bytes + p->work_bytes);
     return NW_OK;
 }
 

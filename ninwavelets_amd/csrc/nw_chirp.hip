@@ -25,8 +25,11 @@
 namespace nw {
 namespace {
 
-// signals per block; measured (n = 1201 / 4097): 4 -2 % / -1 %, 16 +0.6 % / +0.6 % (noise)
+// signals per block; measured (n = 1201 / 4097): 4 -2 % / -1 %, 16 +0.6 % / +0.6 % (noise).
+// The partial-sum form writes one row per block: execute_reduce sizes and accumulates them by
+// fused_psum_groups, i.e. kPsumGroup signals per row
 constexpr int kGroupC = 8;
+static_assert(kGroupC == kPsumGroup, "chirp-z partial rows are counted by fused_psum_groups");
 constexpr int kTileFC = 8;    // scales per XCD tile
 constexpr int kTileGC = 4;    // signal groups per XCD tile
 constexpr int kRegOsz = 16;   // PassInfo without last-pass pairing: j = t + q*T everywhere

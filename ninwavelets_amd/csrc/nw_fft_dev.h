@@ -282,19 +282,28 @@ __device__ __forceinline__ typename OutT<OUT, T>::type out_value(C2<T> y) {
 // write of the store's data VGPRs in the very next instruction (which the compiler does not
 // guard for that form) corrupted the first dword of 16-B stores on gfx950.
 constexpr int kStoreGlobal = 0, kStoreGlobalNt = 1, kStoreBuffer = 2;
+// (NW_LINT_HAZARD_SOFFSET: the old, hazardous form with the offset in the soffset field --
+// built only by tests/test_isa_lint.py, device code only and never run, to show that
+// tools/isa_lint.py catches it)
+#ifdef NW_LINT_HAZARD_SOFFSET
+constexpr bool kSoffsetInField = true;
+#else
+constexpr bool kSoffsetInField = false;
+#endif
 template <int SP, typename V>
 __device__ __forceinline__ void store_row(V val, void* row, uint32_t lane_off, uint32_t c_off) {
     if constexpr (SP == kStoreBuffer) {
-        const __amdgpu_buffer_rsrc_t rs =
-            __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<char*>(row) + c_off, 0, 0x7fffffff, 0x00020000);
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<char*>(row) + (kSoffsetInField ? 0 : c_off), 0, 0x7fffffff, 0x00020000);
+        const int so = kSoffsetInField ? (int)c_off : 0;
         if constexpr (sizeof(V) == 16)
             __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, val),
-                                                   rs, (int)lane_off, 0, 2);
+                                                   rs, (int)lane_off, so, 2);
         else if constexpr (sizeof(V) == 8)
             __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(__attribute__((ext_vector_type(2))) unsigned, val),
-                                                  rs, (int)lane_off, 0, 2);
+                                                  rs, (int)lane_off, so, 2);
         else
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs, (int)lane_off, 0, 2);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, val), rs, (int)lane_off, so, 2);
     } else {
         __builtin_nontemporal_store(val, reinterpret_cast<V*>(at(reinterpret_cast<char*>(row), lane_off, c_off)));
     }

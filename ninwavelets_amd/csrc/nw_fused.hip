@@ -73,11 +73,8 @@ constexpr int kWKeep32 = 16, kWKeep32Small = 8;
 // E = 32: a pass-0 variant for rows whose support ends below 3/4 of n (NZ = 24: C4's rows
 // above 186 Hz), between the power-of-two variants: C4 3.360-3.368 -> 3.346-3.351 ms
 constexpr bool kNz24 = true;
-// signal-pair kernel: the next pair's X by LDS-DMA before the stores
-#ifndef NW_PAIR_XD
-#define NW_PAIR_XD 1
-#endif
-constexpr bool kPairXD = NW_PAIR_XD;
+// signal-pair kernel: the next pair's X by LDS-DMA before the stores (cwt output only, below)
+constexpr bool kPairXD = true;
 template <typename T, int N, int E> constexpr bool kNz24Of = kNz24 && E > 16;
 // NZ = 12 and 20 between them (fp32 only: fp64 n = 16384 |y| spills 20 B with them)
 template <typename T, int N, int E> constexpr bool kNzFineOf = kNz24Of<T, N, E> && sizeof(T) == 4;
@@ -87,10 +84,8 @@ template <typename T, int N, int E> constexpr bool kNzFineOf = kNz24Of<T, N, E> 
 // the Infinity Cache); the C4 shape in fp64 10.04 -> 9.66 ms per launch (2 / 3 signals:
 // 9.55 / 9.40, 16: 9.71; two boxes, tools/ab.sh)
 constexpr int kGroup = 8;
-#ifndef NW_GROUP64
-#define NW_GROUP64 4
-#endif
-constexpr int kGroup64 = NW_GROUP64;
+static_assert(kGroup == kPsumGroup, "fused partial rows are counted by fused_psum_groups");
+constexpr int kGroup64 = 4;
 // XCD tile: kTileF scales x kTileG signal groups per XCD round (fp64 tiles 16 x 2, 4 x 8,
 // 32 x 1, 2 x 16 measured -2.4 / -0.2 / -4.8 / -3.5 % against 8 x 4)
 constexpr int kTileF = 8, kTileG = 4;
@@ -117,6 +112,11 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     using G = Geometry<N, E>;
     using WT = typename WLoad<T, REALW>::type;
     constexpr bool XD = kXDMA<T, E, REALW>;
+    // the LDS-DMA copies dma_rounds_for(nzv) rounds of the bins pass-0 variant nzv reads; with a
+    // shifted support table (WSH > 0: nz = wnz >> WSH can be 6 or 10, between the variants) it
+    // would copy fewer bins than the dispatched variant reads.  The shift only occurs for the
+    // E = 16 partial-sum kernels, which never DMA (kXdmaMinE = 32)
+    static_assert(!XD || WSH == 0, "X LDS-DMA needs the unshifted W-support table");
     extern __shared__ __align__(16) unsigned char smem[];
     T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
@@ -412,9 +412,7 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
         };
         if (nz <= 4) pass0.template operator()<4>();
         else if (nz <= 8) pass0.template operator()<8>();
-#ifndef NW_NO_NZ12
         else if (nz <= 12) pass0.template operator()<12>();
-#endif
         else pass0.template operator()<E>();
         void* o1 = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;
         void* o2 = two ? (void*)((char*)out + (s2 * d.nfreq + fi) * (int64_t)N * out_esz) : nullptr;

@@ -192,6 +192,10 @@ hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 p
 // or with phase of y / |y|; one
 // (groups, F, n) row of fp64 (phase: complex fp64) per (group, scale);
 // groups = fused_psum_groups(nsig)
+// Signals per partial-sum row: the block size of both the fused kernels (kGroup) and the
+// chirp-z kernel (kGroupC), each static_assert'ed equal to it, so one fused_psum_groups sizes
+// and accumulates the partial rows of either form
+constexpr int kPsumGroup = 8;
 bool fused_psum_supported(int64_t n, int dtype, int kind, bool phase);
 int64_t fused_psum_groups(int64_t nsig);
 int fused_psum_kernel_id(int64_t n, int dtype, bool phase);   // NW_K_FUSED or NW_K_FUSED_PAIR

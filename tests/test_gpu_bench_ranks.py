@@ -43,8 +43,10 @@ def test_two_ranks_share_the_gpu_with_kernels():
 
 
 def test_c4_line_carries_an_fp64_leg():
-    d, _ = run_bench('--config', 'c4', '--epochs', '2', '--steps', '1', '--warmup', '1', '--no-cpu-baseline')
+    d, _ = run_bench('--config', 'c4', '--epochs', '2', '--steps', '1', '--warmup', '1', '--no-cpu-baseline',
+                     '--legs', 'fp64')
     assert d['dtype'] == 'f32' and d['roofline']['kernel'] == 'nw_fused_kernel'
+    assert 'c3' not in d and 'c5' not in d
     f = d['fp64']
     assert f['dtype'] == 'f64' and f['value'] > 0 and 'complex128' in f['workload']
     assert f['roofline']['kernel'] == 'nw_fused_kernel' and f['roofline']['frac'] > 0
@@ -52,3 +54,27 @@ def test_c4_line_carries_an_fp64_leg():
     assert f['roofline']['algorithmic_bytes_per_launch'] == pytest.approx(
         2 * d['roofline']['algorithmic_bytes_per_launch'])
     assert f['valu_roofline']['peak'] == 78.6
+
+
+def test_default_line_carries_c3_and_c5_legs():
+    """BASELINE.json's C3 (fused |.|^2, base.py:409-425) and C5 (2^24 samples x 512 scales,
+    fp32 and fp64, base.py:404-406) ride on the default line with their own rooflines."""
+    d, _ = run_bench('--config', 'c4', '--epochs', '2', '--steps', '1', '--warmup', '1', '--no-cpu-baseline',
+                     '--legs', 'c3,c5,c5_fp64', timeout=600)
+    assert d['fp64'] is None
+    c3 = d['c3']
+    assert c3['dtype'] == 'f32' and c3['output'] == 'power' and c3['value'] > 0
+    assert c3['roofline']['kernel'] == 'nw_fused_pair_kernel' and c3['roofline']['frac'] > 0
+    # --epochs scales C3's epochs down: 2 epochs x 64 ch x 4096 x 256 per step
+    assert c3['value'] == pytest.approx(2 * 64 * 4096 * 256 / (c3['ms_per_step'] * 1e-3), rel=1e-9)
+    assert c3['valu_roofline']['kernel'] == 'nw_fused_pair_kernel'
+    for key, dt, peak in (('fp32', 'f32', 157.3), ('fp64', 'f64', 78.6)):
+        c5 = d['c5'][key]
+        assert c5['dtype'] == dt and c5['output'] == 'cwt'
+        assert c5['roofline']['kernel'] == 'cols_kernel' and c5['roofline_rows']['kernel'] == 'rows_kernel'
+        assert c5['value'] == pytest.approx((1 << 24) * 512 / (c5['ms_per_step'] * 1e-3), rel=1e-9)
+        esz = 4 if dt == 'f32' else 8
+        # end to end against X once + every output once
+        assert c5['end_to_end_min_traffic']['bytes_per_step'] == pytest.approx(
+            ((1 << 23) + 1) * 2 * esz + 512 * (1 << 24) * 2 * esz)
+        assert c5['valu_roofline']['peak'] == peak

@@ -223,3 +223,24 @@ def test_chirp_fused_epoch_partials(dtype, n):
     assert within(pm[::51], np.mean(np.abs(o) ** 2, axis=0), dtype, 'power')
     t_itc = 1e-10 if dtype == 'float64' else 1e-4
     assert np.max(np.abs(itc[::51] - np.abs(np.mean(o / np.abs(o), axis=0)))) <= t_itc
+
+
+@pytest.mark.parametrize('dtype', ['float64', 'float32'])
+def test_chirp_table_rows_epoch_reductions(dtype):
+    """Epoch reductions of complex table rows (MexicanHat: base.py:249-256, WaveletMode.Normal)
+    at an MNE length on the chirp-z form (mneutils.py:42-71).  Table rows take the per-signal
+    chunk path (their partial-sum kernels are not scratch-free), so power_sum equals the sum of
+    the same plan's power output and ITC the materialised cwt's, both against the oracle."""
+    n, S = 1201, 11
+    freqs = np.arange(1, 100, 7, dtype=np.float64)
+    x = synth(S, n, seed=4242).astype(dtype)
+    w = nw.MexicanHat(1000, dtype=dtype)
+    pm = w.cwt_batch(x, freqs, out='power_mean')
+    assert w._plans and all(pl.stats()['engine'] == 'fused' for pl in w._plans.values())
+    c = w.cwt_batch(x, freqs).astype(np.complex128)
+    assert L.KERNEL_NAMES[next(iter(w._plans.values())).stats()['kernel']] == 'nw_chirp_kernel'
+    np.testing.assert_allclose(pm, np.mean(np.abs(c) ** 2, axis=0), rtol=1e-12 if dtype == 'float64' else 1e-5)
+    itc = w.cwt_batch(x, freqs, out='itc')
+    assert np.max(np.abs(itc - np.abs(np.mean(c / np.abs(c), axis=0)))) <= (1e-12 if dtype == 'float64' else 1e-5)
+    o = oracle('mexican_hat', x, freqs, 'cwt')
+    assert within(pm, np.mean(np.abs(o) ** 2, axis=0), dtype, 'power')

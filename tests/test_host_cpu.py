@@ -194,3 +194,33 @@ def test_debug_library_builds_and_exports():
         assert hasattr(lib, name), name
     assert L.lib().nw_debug_bounds() == 0
     assert L.lib().nw_debug_selftest(0) == L.NW_E_STATE
+
+
+def test_plan_cache_evicts_least_recently_used():
+    """WaveletBase._evict_plans (no GPU: stand-in plans report their device bytes): the least
+    recently used plans are closed until the cache fits plan_cache_bytes; the current call's
+    plans stay even when they alone exceed it."""
+    from collections import OrderedDict
+
+    class FakePlan:
+        def __init__(self, b):
+            self.b, self.closed = b, False
+
+        def stats(self):
+            return {'device_bytes': self.b}
+
+        def close(self):
+            self.closed = True
+
+    w = nw.Morse(1000)
+    plans = [FakePlan(b) for b in (10, 20, 30, 40)]
+    w._plans = OrderedDict((i, p) for i, p in enumerate(plans))
+    w.plan_cache_bytes = 75
+    w._evict_plans(keep=1)
+    assert list(w._plans) == [2, 3] and plans[0].closed and plans[1].closed and not plans[2].closed
+    w.plan_cache_bytes = 5
+    w._evict_plans(keep=1)
+    assert list(w._plans) == [3] and not plans[3].closed
+    w._plans = OrderedDict((i, p) for i, p in enumerate([FakePlan(50), FakePlan(50)]))
+    w._evict_plans(keep=2)                      # a two-device call keeps both of its plans
+    assert len(w._plans) == 2

@@ -10,7 +10,7 @@ R=$1; REPS=$2; BARGS=$3; shift 3
 mkdir -p $R
 for rep in $(seq 1 $REPS); do for v in "$@"; do
   lib=$PWD/ninwavelets_amd/libninwave_$v.so; [ "$v" = base ] && lib=$PWD/ninwavelets_amd/libninwave.so
-  NINWAVE_LIB=$lib timeout -k 10 300 python bench.py $BARGS --no-cpu-baseline --no-fp64 > $R/$v-$rep.json 2> $R/$v-$rep.log || { echo "FAIL $v rep$rep"; tail -5 $R/$v-$rep.log; exit 1; }
+  NINWAVE_LIB=$lib timeout -k 10 300 python bench.py $BARGS --no-cpu-baseline --legs none > $R/$v-$rep.json 2> $R/$v-$rep.log || { echo "FAIL $v rep$rep"; tail -5 $R/$v-$rep.log; exit 1; }
   python3 - "$R/$v-$rep.json" "$v" "$rep" <<'PY'
 import json, sys
 d = json.load(open(sys.argv[1])); r = d['roofline']; rr = d.get('roofline_rows') or {}

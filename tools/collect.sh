@@ -5,8 +5,8 @@
 set -eu
 R=${1:-gpurun_out/rec}
 P=profiles
-ROUND=${ROUND:-r03}
-for c in ${CFGS:-c4 c3 c5 c4f64}; do
+ROUND=${ROUND:-r04}
+for c in ${CFGS:-c4 c3 c5 c5f64 c4f64}; do
   [ -s $R/bench_$c.json ] || { echo "no bench line for $c"; continue; }
   cp $R/bench_$c.json $P/${ROUND}_bench_$c.json
   st=$(find $R/prof_$c -name '*kernel_stats.csv' | head -1)
@@ -14,7 +14,7 @@ for c in ${CFGS:-c4 c3 c5 c4f64}; do
   for j in $R/pmc_${c}_*.json; do
     [ -e "$j" ] || continue
     k=${j#$R/pmc_${c}_}
-    case $c in c4f64) dst=$P/pmc_c4_f64_$k ;; *) dst=$P/pmc_${c}_$k ;; esac
+    case $c in c4f64) dst=$P/pmc_c4_f64_$k ;; c5f64) dst=$P/pmc_c5_f64_$k ;; *) dst=$P/pmc_${c}_$k ;; esac
     cp "$j" "$dst"
   done
   echo "collected $c"
