@@ -750,7 +750,15 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
 
 // ---- host-buffer copy-out: pinned double-buffered pieces + a multi-threaded host copy
 constexpr size_t kPiece = size_t(64) << 20;
-constexpr int kCopyThreads = 8;
+// host copy threads (NW_COPY_THREADS overrides, diagnostics)
+int copy_threads() {
+    static const int n = [] {
+        const char* e = std::getenv("NW_COPY_THREADS");
+        const int v = e ? std::atoi(e) : 8;
+        return v > 0 ? v : 8;
+    }();
+    return n;
+}
 
 int copy_out(nw_plan* p, char* dst, const char* src, size_t bytes) {
     if (!p->pinned[0]) {
@@ -771,7 +779,7 @@ int copy_out(nw_plan* p, char* dst, const char* src, size_t bytes) {
             const size_t k = i - 1, off = k * kPiece;
             NW_HIP(hipEventSynchronize(p->pinned_ev[k & 1]));
             nw::host::parallel_copy(dst + off, (const char*)p->pinned[k & 1], std::min(kPiece, bytes - off),
-                                   kCopyThreads);
+                                   copy_threads());
         }
     }
     return NW_OK;
@@ -1253,9 +1261,9 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     if (host && p->engine == NW_ENGINE_FUSED) NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * row_out));
     if (host && p->engine == NW_ENGINE_ROCFFT && out_kind == NW_OUT_CWT) NW_TRY(need_Y(p));
     // (rocFFT engine, host CWT: the complex result is read back straight from d_Y)
-    // a fresh host array (the reference returns a new one per call) is populated in parallel
-    // first, on huge pages where the kernel grants them, instead of page by page in the copy
-    if (host) nw::host::prefault_output((char*)out, (size_t)nsig * row_out, kCopyThreads);
+    // a fresh host array (the reference returns a new one per call) faults in on huge pages
+    // where the kernel grants them, not 4 KiB at a time inside the copy-out
+    if (host) nw::host::advise_output((char*)out, (size_t)nsig * row_out);
 
     for (int64_t s0 = 0; s0 < nsig; s0 += p->max_batch) {
         const int64_t c = std::min<int64_t>(p->max_batch, nsig - s0);

@@ -2,19 +2,13 @@
 #include "nw_host.h"
 
 #include <sys/mman.h>
-#include <unistd.h>
 
 #include <algorithm>
-#include <cerrno>
 #include <cmath>
 #include <cstring>
 #include <map>
 #include <thread>
 #include <unordered_map>
-
-#ifndef MADV_POPULATE_WRITE
-#define MADV_POPULATE_WRITE 23   // Linux 5.14
-#endif
 
 namespace nw {
 namespace host {
@@ -178,40 +172,13 @@ void parallel_copy(char* dst, const char* src, size_t bytes, unsigned max_thread
     for (auto& t : th) t.join();
 }
 
-namespace {
-// populate [a, a + len) (page-aligned) writable; one volatile write per page when the kernel
-// has no MADV_POPULATE_WRITE (EINVAL): the caller overwrites the whole range afterwards
-void populate(char* a, size_t len, size_t page) {
-    if (len == 0) return;
-    if (madvise(a, len, MADV_POPULATE_WRITE) == 0) return;
-    if (errno != EINVAL) return;          // e.g. not anonymous memory: leave it to the copy
-    for (size_t off = 0; off < len; off += page) *reinterpret_cast<volatile char*>(a + off) = 0;
-}
-}  // namespace
-
-unsigned prefault_output(char* dst, size_t bytes, unsigned max_threads) {
-    const long pg = sysconf(_SC_PAGESIZE);
-    const size_t page = pg > 0 ? (size_t)pg : 4096, huge = size_t(2) << 20;
+size_t advise_output(char* dst, size_t bytes) {
+    const size_t huge = size_t(2) << 20;
     const uintptr_t b = (uintptr_t)dst, e = b + bytes;
-    const uintptr_t pb = (b + page - 1) / page * page, pe = e / page * page;   // whole pages inside
-    if (bytes < huge || pe <= pb) return 0;
     const uintptr_t hb = (b + huge - 1) / huge * huge, he = e / huge * huge;
-    if (he > hb) (void)madvise(reinterpret_cast<void*>(hb), he - hb, MADV_HUGEPAGE);
-    // slices of whole huge pages (a huge page is faulted by one thread), >= 32 MiB each
-    const size_t span = pe - pb, min_share = size_t(32) << 20;
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const size_t nth = std::min<size_t>(std::min<size_t>(std::max(1u, max_threads), hw),
-                                        std::max<size_t>(1, span / min_share));
-    const size_t share = (span / nth + huge - 1) / huge * huge;
-    std::vector<std::thread> th;
-    for (size_t i = 1; i < nth; ++i) {
-        const size_t off = i * share;
-        if (off >= span) break;
-        th.emplace_back([=] { populate(reinterpret_cast<char*>(pb + off), std::min(share, span - off), page); });
-    }
-    populate(reinterpret_cast<char*>(pb), std::min(share, span), page);
-    for (auto& t : th) t.join();
-    return (unsigned)(th.size() + 1);
+    if (bytes < huge || he <= hb) return 0;
+    (void)madvise(reinterpret_cast<void*>(hb), he - hb, MADV_HUGEPAGE);
+    return he - hb;
 }
 
 }  // namespace host

@@ -294,3 +294,51 @@ def make_wavelet(kind: str, freq: float, sfreq: float = 1000., real_wave_length:
 
 def make_wavelets(kind: str, freqs, **kw) -> list:
     return [make_wavelet(kind, f, **kw) for f in freqs]
+
+
+# ---------------------------------------------------------------------------
+# user plugins (README.md:342-355): any WaveletBase subclass, by its mode
+# ---------------------------------------------------------------------------
+
+
+def plugin_row(mode: str, trans_formula, formula, peak_freq, freq: float, sfreq: float,
+               real_length: float, interpolate: bool, real_wave_length: float = 1.) -> np.ndarray:
+    """One cached row of a user plugin: make_fft_wavelet (base.py:221-256) by the plugin's
+    mode name.  Reverse / Both: the spectrum on the trans grid (base.py:238-245, ×2 zero-padded
+    when interpolating); Normal / Twice / Indifferentiable: the FFT of the zero-padded
+    time-domain wavelet, |Re| + i|Im| (base.py:247-256), where make_wavelet (base.py:346-359)
+    takes Twice (and Reverse) through ifft(trans_formula(t)) on the freq's own grid
+    (trans_formula called with its default freq, base.py:350), conj-mirrored, and the others
+    through formula(timeline, freq) on _setup_waveletshape's grid (base.py:196-216)."""
+    if freq == 0:
+        raise ZeroDivisionError
+    if mode in ('Reverse', 'Both'):
+        nu = trans_grid(sfreq, real_length, interpolate)
+        w = trans_formula(nu, freq)
+        return np.hstack((w, np.zeros(len(nu)))) if interpolate else w
+    if mode in ('Reverse', 'Twice'):
+        t = np.arange(0, sfreq / freq * real_wave_length, 1 / freq)          # base.py:191-194
+        w = ifft(trans_formula(t))
+        half = int(w.shape[0])
+        w = np.hstack((np.conj(np.flip(w)), w))[half // 2: half // 2 * 3]
+    else:
+        peak = peak_freq(freq)
+        total = 1 / peak * freq * 2 * np.pi                                   # base.py:211-216
+        one = 1 / sfreq * 2 * np.pi * freq / peak
+        w = formula(np.arange(-total / 2, total / 2, one), freq)
+    half = int((sfreq * real_wave_length - w.shape[0]) / 2)
+    spec = fft(np.hstack((np.zeros(half), w, np.zeros(half))))
+    return np.abs(spec.real) + 1j * np.abs(spec.imag)
+
+
+def plugin_cwt(mode: str, trans_formula, formula, peak_freq, x: np.ndarray, freqs,
+               sfreq: float = 1000., interpolate: bool = False, real_wave_length: float = 1.):
+    """Uncached CWT of one signal with a user plugin (base.py:258-279 then 378-407)."""
+    freqs = list(freqs)
+    if len(freqs) < 2:
+        raise IndexError('freqs needs at least two entries (base.py:272)')
+    rows = [plugin_row(mode, trans_formula, formula, peak_freq, f, sfreq, x.shape[0] / sfreq, interpolate,
+                       real_wave_length) for f in freqs]
+    if interpolate:
+        rows = [alias_mask(r) for r in rows]
+    return cwt_from_rows(x, rows, interpolate), rows

@@ -1,6 +1,6 @@
 // CPU driver for the sanitizer build of the engine's host-only logic (nw_host.cpp):
 // built with -fsanitize=address,undefined by tests/test_host_asan.py.
-//   host_asan self      : invariant checks of group_rows / block_of / parallel_copy / prefault_output /
+//   host_asan self      : invariant checks of group_rows / block_of / parallel_copy / advise_output /
 //                         normal_rows
 //   host_asan grid      : stdin "real_length sfreq interpolate" -> "len_valid len_full delta"
 #include <cstdio>
@@ -107,19 +107,18 @@ static void self_checks() {
             parallel_copy(dst.data(), src.data(), bytes, th);
             CHECK(std::memcmp(dst.data(), src.data(), bytes) == 0);
         }
-    // prefault_output: contents kept, whole range writable afterwards, odd bounds and sizes
+    // advise_output: contents kept, whole range writable afterwards, odd bounds and sizes
     for (size_t bytes : {size_t(0), size_t(100), (size_t(2) << 20) - 1, (size_t(37) << 20) + 11,
-                         (size_t(130) << 20) + 4097})
-        for (unsigned th : {0u, 1u, 3u, 8u}) {
-            std::vector<char> buf(bytes + 64);
-            char* dst = buf.data() + 5;                  // not page aligned
-            for (size_t i = 0; i < bytes; i += 4093) dst[i] = (char)(i * 7 + th);
-            const unsigned used = prefault_output(dst, bytes, th);
-            CHECK(used <= (th ? th : 1u) + 0u || used == 1u);
-            CHECK(bytes >= (size_t(2) << 20) || used == 0);
-            for (size_t i = 0; i < bytes; i += 4093) CHECK(dst[i] == (char)(i * 7 + th));
-            std::memset(dst, 1, bytes);
-        }
+                         (size_t(130) << 20) + 4097}) {
+        std::vector<char> buf(bytes + 64);
+        char* dst = buf.data() + 5;                      // not page aligned
+        for (size_t i = 0; i < bytes; i += 4093) dst[i] = (char)(i * 7);
+        const size_t adv = advise_output(dst, bytes);
+        CHECK(adv <= bytes && adv % (size_t(2) << 20) == 0);
+        CHECK(bytes >= (size_t(4) << 20) || adv <= (size_t(2) << 20));
+        for (size_t i = 0; i < bytes; i += 4093) CHECK(dst[i] == (char)(i * 7));
+        std::memset(dst, 1, bytes);
+    }
     // normal_rows: offsets tile the batched buffer, rows of equal length consecutive
     for (int mh = 0; mh < 2; ++mh) {
         const double params[3] = {7.0, 1000.0, 1.0};

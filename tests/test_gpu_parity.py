@@ -19,7 +19,8 @@ import ninwavelets_amd as nw  # noqa: E402
 
 TOL = {'float64': 1e-12, 'float32': 1e-5}
 ENGINES = ['rocfft', 'auto']
-SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets', 'long'))]
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets', 'long',
+                                                          'plugin'))]
 CLASSES = {'morse': nw.Morse, 'morlet': nw.Morlet, 'shannon': nw.Shannon,
            'mexican_hat': nw.MexicanHat, 'haar': nw.Haar}
 

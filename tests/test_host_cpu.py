@@ -224,3 +224,18 @@ def test_plan_cache_evicts_least_recently_used():
     w._plans = OrderedDict((i, p) for i, p in enumerate([FakePlan(50), FakePlan(50)]))
     w._evict_plans(keep=2)                      # a two-device call keeps both of its plans
     assert len(w._plans) == 2
+
+
+@pytest.mark.parametrize('name', golden_names('plugin_'))
+def test_plugin_rows_are_the_references(name):
+    """User plugins (README.md:342-355) on the drop-in: the cached rows the host evaluates with
+    the plugin's own formula equal the reference's make_fft_wavelets rows bit for bit
+    (base.py:221-279; Reverse, Morse-subclass, Normal and Twice plugins, tests/plugins.py)."""
+    import plugins
+    g = load_golden(name)
+    m = g['meta']
+    w = plugins.make(nw, m['plugin'], m['sfreq'], m['interpolate'])
+    rows = w.make_fft_wavelets(list(g['freqs']), m['n'] / m['sfreq'])
+    np.testing.assert_array_equal(rows[0], g['w_first'])
+    np.testing.assert_array_equal(rows[-1], g['w_last'])
+    assert w._cache.kind == 'table'           # plugins take the host-table path

@@ -7,7 +7,8 @@ import pytest
 from conftest import golden_names, load_golden
 from oracle import nw_oracle as O
 
-SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets', 'long'))]
+SINGLE = [n for n in golden_names() if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets', 'long',
+                                                          'plugin'))]
 
 
 def _params(meta):
@@ -108,3 +109,21 @@ def test_oracle_matches_reference_at_benchmark_lengths(name):
     np.testing.assert_allclose(out.sum(axis=1), g['row_sum'], rtol=0,
                                atol=1e-13 * np.max(np.abs(g['row_sum'])))
     np.testing.assert_allclose((np.abs(out) ** 2).sum(axis=1), g['row_energy'], rtol=1e-13)
+
+
+@pytest.mark.parametrize('name', golden_names('plugin_'))
+def test_oracle_plugins(name):
+    """User plugins (README.md:342-355; tests/plugins.py) through the oracle's generic
+    make_fft_wavelet (base.py:221-256, 346-359) against the reference's own outputs."""
+    import ninwavelets_amd
+    import plugins
+    g = load_golden(name)
+    m = g['meta']
+    w = plugins.make(ninwavelets_amd, m['plugin'], m['sfreq'], m['interpolate'])
+    assert w.mode.name == m['mode']
+    out, rows = O.plugin_cwt(m['mode'], w.trans_formula, w.formula, w.peak_freq, g['x'], g['freqs'],
+                             sfreq=m['sfreq'], interpolate=m['interpolate'])
+    np.testing.assert_array_equal(rows[0], g['w_first'])
+    np.testing.assert_array_equal(rows[-1], g['w_last'])
+    assert np.max(np.abs(out - g['out'])) <= 1e-15 * np.max(np.abs(g['out']))
+    assert np.max(np.abs(np.abs(out) ** 2 - g['power'])) <= 1e-15 * np.max(g['power'])

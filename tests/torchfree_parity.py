@@ -49,7 +49,7 @@ def rel(got, ref):
 
 def single_goldens():
     names = [n for n in golden_names()
-             if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets', 'long'))]
+             if not n.startswith(('readme_2d', 'reuse', 'epochs', 'baseline', 'wavelets', 'long', 'plugin'))]
     for name in names:
         g = load_golden(name)
         m = g['meta']
