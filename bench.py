@@ -315,7 +315,7 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name, dtype
     def barrier():
         torch.cuda.synchronize()
         plan.sync()
-        if world > 1:
+        if dist.is_initialized():
             dist.barrier()
 
     log(f'[bench] rank {rank}/{world} {cfg_name}{" fp64 leg" if fp64_leg else ""}: S={S} n={n} F={F} '
@@ -331,7 +331,7 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name, dtype
         step()
     barrier()
     el = time.perf_counter() - t0
-    el = max_over_ranks(torch, dist, el, world, dev if backend == 'nccl' else None)
+    el = max_over_ranks(torch, dist, el, dev if backend == 'nccl' else None)
     st = plan.stats()
     points = float(S) * F_all * n * args.steps * (1 if by_scales else world)
     res = {'value': points / el, 'ms_per_step': el / args.steps * 1e3, 'dtype': 'f64' if f64 else 'f32',
@@ -527,7 +527,9 @@ def main(argv=None):
 
     if args.same_device:
         local = local % max(1, torch.cuda.device_count())
-    if world > 1:
+    # a process group whenever there are several ranks, or one rank launched by torchrun with
+    # an explicit --backend (the driver's N-GPU path, RCCL included, at N = 1)
+    if world > 1 or (args.backend is not None and 'MASTER_ADDR' in os.environ):
         torch.cuda.set_device(local)
         if backend == 'nccl':
             dist.init_process_group('nccl', device_id=torch.device('cuda', local), timeout=timeout)
@@ -581,19 +583,20 @@ def main(argv=None):
                        'parallelism': (f'scales{world} (each rank a contiguous slice of the scales, '
                                        f'no collective)' if res['by_scales'] else
                                        f'dp{world} (signals sharded, no collective)'),
-                       **({'backend': backend, 'same_device': True} if args.same_device else {})},
+                       **({'backend': backend, 'same_device': True} if args.same_device else {}),
+                       **({'process_group': dist.get_backend()} if dist.is_initialized() else {})},
             'roofline': roof, **extra, 'fp64': fp64, **leg_out, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool,
             'stage_ms_per_step': stage_ms,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
     return 0
 
 
-def max_over_ranks(torch, dist, el, world, device):
+def max_over_ranks(torch, dist, el, device):
     """The step time the job took: the MAX of every rank's elapsed time."""
-    if world <= 1:
+    if not dist.is_initialized():
         return el
     t = torch.tensor([el], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -623,7 +626,7 @@ def dry_run(args, torch, dist, world, rank, backend, timeout=None):
     for _ in range(args.steps):
         step()
     barrier()
-    el = max_over_ranks(torch, dist, time.perf_counter() - t0, world, None)
+    el = max_over_ranks(torch, dist, time.perf_counter() - t0, None)
     if rank == 0:
         print(json.dumps({
             'metric': 'CWT throughput (epochs*chans*samples*freqs)/s', 'value': None, 'unit': 'points/s',

@@ -263,6 +263,14 @@ int nw_baseline(int device, int dtype, const void* x, int64_t count, int64_t row
 int nw_make_wavelets(int device, int kind, const double* params, int nparams, const double* freqs, int nfreq,
                      double sfreq, double real_wave_length, void* out, int64_t* max_len, int64_t* row_len);
 
+/* Page-locked host memory for results (no reference counterpart: the drop-in classes pool
+ * their result arrays in it, ninwavelets_amd/engine.py HostPool).  nw_execute with
+ * NW_MEM_HOST writes an output that lies inside such an allocation by DMA directly, without
+ * the staging copy; a fresh pageable array instead is faulted in page by page during the
+ * copy-out.  nw_host_free takes exactly a pointer nw_host_alloc returned. */
+int nw_host_alloc(int64_t bytes, void** ptr);
+int nw_host_free(void* ptr);
+
 int nw_plan_set_stream(nw_plan* plan, void* hip_stream);   /* NULL: the plan's own stream */
 /* The hipStream_t the plan currently launches on (for event ordering with the caller's
  * streams: device-buffer executes are asynchronous on it). */

@@ -93,6 +93,8 @@ SIGNATURES = [
                                         ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_double,
                                         ctypes.c_double, _P, ctypes.POINTER(ctypes.c_int64),
                                         ctypes.POINTER(ctypes.c_int64)]),
+    ('nw_host_alloc', ctypes.c_int, [_I64, ctypes.POINTER(_P)]),
+    ('nw_host_free', ctypes.c_int, [_P]),
     ('nw_plan_set_stream', ctypes.c_int, [_P, _P]),
     ('nw_plan_get_stream', ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     ('nw_plan_sync', ctypes.c_int, [_P]),

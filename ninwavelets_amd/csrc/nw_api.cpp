@@ -748,6 +748,19 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     return NW_OK;
 }
 
+// ---- page-locked result buffers (nw_host_alloc): a destination inside one is written by DMA
+std::mutex g_host_mu;
+std::map<uintptr_t, size_t> g_host_bufs;   // base -> bytes
+
+bool host_pinned(const void* p, size_t bytes) {
+    const uintptr_t a = (uintptr_t)p;
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host_bufs.upper_bound(a);
+    if (it == g_host_bufs.begin()) return false;
+    --it;
+    return a >= it->first && a + bytes <= it->first + it->second;
+}
+
 // ---- host-buffer copy-out: pinned double-buffered pieces + a multi-threaded host copy
 constexpr size_t kPiece = size_t(64) << 20;
 // host copy threads (NW_COPY_THREADS overrides, diagnostics)
@@ -1261,9 +1274,11 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     if (host && p->engine == NW_ENGINE_FUSED) NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * row_out));
     if (host && p->engine == NW_ENGINE_ROCFFT && out_kind == NW_OUT_CWT) NW_TRY(need_Y(p));
     // (rocFFT engine, host CWT: the complex result is read back straight from d_Y)
-    // a fresh host array (the reference returns a new one per call) faults in on huge pages
-    // where the kernel grants them, not 4 KiB at a time inside the copy-out
-    if (host) nw::host::advise_output((char*)out, (size_t)nsig * row_out);
+    // a page-locked destination (nw_host_alloc) is written by DMA directly; a fresh pageable
+    // array (the reference returns a new one per call) faults in on huge pages where the
+    // kernel grants them, not 4 KiB at a time inside the copy-out
+    const bool direct = host && host_pinned(out, (size_t)nsig * row_out);
+    if (host && !direct) nw::host::advise_output((char*)out, (size_t)nsig * row_out);
 
     for (int64_t s0 = 0; s0 < nsig; s0 += p->max_batch) {
         const int64_t c = std::min<int64_t>(p->max_batch, nsig - s0);
@@ -1276,7 +1291,13 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
             }));
             void* dst = (p->engine == NW_ENGINE_ROCFFT && out_kind == NW_OUT_CWT) ? p->d_Y : p->d_out;
             NW_TRY(run_chunk(p, p->d_x, c, dst, out_kind, true));
-            NW_TRY(staged(p, ST_COPY, [&] { return copy_out(p, os, (const char*)dst, (size_t)c * row_out); }));
+            NW_TRY(staged(p, ST_COPY, [&] {
+                if (direct) {
+                    NW_HIP(hipMemcpyAsync(os, dst, (size_t)c * row_out, hipMemcpyDeviceToHost, p->stream));
+                    return NW_OK;
+                }
+                return copy_out(p, os, (const char*)dst, (size_t)c * row_out);
+            }));
             NW_HIP(hipStreamSynchronize(p->stream));
         } else {
             NW_TRY(run_chunk(p, xs, c, os, out_kind, true));
@@ -1690,6 +1711,26 @@ int nw_plan_set_stream(nw_plan* p, void* stream) {
 int nw_plan_get_stream(nw_plan* p, void** stream) {
     if (!p || !stream) return fail(NW_E_INVALID, "nw_plan_get_stream: null argument");
     *stream = (void*)p->stream;
+    return NW_OK;
+}
+
+int nw_host_alloc(int64_t bytes, void** ptr) {
+    if (!ptr || bytes <= 0) return fail(NW_E_INVALID, "nw_host_alloc: bad argument");
+    *ptr = nullptr;
+    NW_HIP(hipHostMalloc(ptr, (size_t)bytes, hipHostMallocDefault));
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_bufs[(uintptr_t)*ptr] = (size_t)bytes;
+    return NW_OK;
+}
+
+int nw_host_free(void* ptr) {
+    {
+        std::lock_guard<std::mutex> lk(g_host_mu);
+        auto it = g_host_bufs.find((uintptr_t)ptr);
+        if (it == g_host_bufs.end()) return fail(NW_E_INVALID, "nw_host_free: not an nw_host_alloc pointer");
+        g_host_bufs.erase(it);
+    }
+    NW_HIP(hipHostFree(ptr));
     return NW_OK;
 }
 

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import contextlib
 import ctypes
+import os
 
 import numpy as np
 
@@ -42,6 +43,95 @@ def out_dtype(dtype, out_kind: str) -> np.dtype:
     if out_kind == 'cwt':
         return np.dtype(np.complex64 if dt == np.float32 else np.complex128)
     return dt
+
+
+class HostPool:
+    """Page-locked result arrays, recycled (nw_host_alloc).
+
+    The reference returns a new array per call (base.py:378-407).  A fresh pageable numpy
+    array of a large result is faulted in page by page while the copy-out writes it, which
+    bounded the host path at a third of the PCIe rate; a page-locked destination is written
+    by DMA directly.  A pooled result is an ordinary numpy array owning its buffer: when the
+    caller drops it (and every view of it), the buffer returns to the pool for the next
+    result of the same size.  At most ``cap`` bytes are page-locked at a time (results the
+    caller keeps count too); past that, results fall back to np.empty.  ``min_bytes``: smaller
+    results are not worth a page-locked buffer."""
+
+    def __init__(self, cap: int, min_bytes: int = 32 << 20, keep_free: int = 2, alloc=None, free=None):
+        import threading
+        self.cap, self.min_bytes, self.keep_free = int(cap), int(min_bytes), int(keep_free)
+        self._alloc, self._free_fn = alloc or self._nw_alloc, free or self._nw_free
+        self._lock = threading.Lock()
+        self._free: dict = {}            # nbytes -> [ptr]
+        self.held = 0                    # page-locked bytes, in use or free
+
+    @staticmethod
+    def _nw_alloc(nbytes):
+        p = ctypes.c_void_p()
+        L.check(L.lib().nw_host_alloc(int(nbytes), ctypes.byref(p)))
+        return p.value
+
+    @staticmethod
+    def _nw_free(ptr):
+        L.check(L.lib().nw_host_free(ctypes.c_void_p(ptr)))
+
+    def free_bytes(self) -> int:
+        return sum(n * len(v) for n, v in self._free.items())
+
+    def _take(self, nbytes):
+        with self._lock:
+            lst = self._free.get(nbytes)
+            if lst:
+                return lst.pop()
+            # make room: drop free buffers of other sizes first
+            for n in list(self._free):
+                while self._free[n] and self.held + nbytes > self.cap:
+                    self._free_fn(self._free[n].pop())
+                    self.held -= n
+            if self.held + nbytes > self.cap:
+                return None
+            self.held += nbytes
+        try:
+            return self._alloc(nbytes)
+        except Exception:
+            with self._lock:
+                self.held -= nbytes
+            return None
+
+    def _release(self, ptr, nbytes):
+        with self._lock:
+            lst = self._free.setdefault(nbytes, [])
+            if len(lst) < self.keep_free:
+                lst.append(ptr)
+                return
+            self.held -= nbytes
+        self._free_fn(ptr)
+
+    def empty(self, shape, dtype) -> np.ndarray:
+        """np.empty(shape, dtype), page-locked when large enough and within the cap."""
+        import weakref
+        dt = np.dtype(dtype)
+        nbytes = int(np.prod(shape, dtype=np.int64)) * dt.itemsize
+        if nbytes < self.min_bytes:
+            return np.empty(shape, dtype=dt)
+        ptr = self._take(nbytes)
+        if ptr is None:
+            return np.empty(shape, dtype=dt)
+        owner = _PooledBuffer(ptr, tuple(int(s) for s in shape), dt)
+        f = weakref.finalize(owner, self._release, ptr, nbytes)
+        f.atexit = False                 # the process is ending: the OS reclaims it
+        return np.asarray(owner)
+
+
+class _PooledBuffer:
+    """Owner of one pooled buffer: exposes it to numpy (__array_interface__); every array or
+    view made from it keeps it alive."""
+
+    def __init__(self, ptr, shape, dtype):
+        self.__array_interface__ = {'data': (ptr, False), 'shape': shape, 'typestr': dtype.str, 'version': 3}
+
+
+HOST_POOL = HostPool(int(os.environ.get('NINWAVE_HOST_POOL_BYTES', str(8 << 30))))
 
 
 def _is_device_tensor(a) -> bool:
@@ -132,7 +222,7 @@ class Plan:
         odt = out_dtype(self.dtype, out_kind)
         shape = (self.nfreq, self.n) if reduce else lead + (self.nfreq, self.n)
         if out is None:
-            out = np.empty(shape, dtype=odt)
+            out = HOST_POOL.empty(shape, odt)
         elif out.dtype != odt or not out.flags.c_contiguous or out.size != int(np.prod(shape)):
             raise ValueError('out must be a C-contiguous array of the right dtype and size')
         L.check(L.lib().nw_execute(self._h, x.ctypes.data_as(ctypes.c_void_p), nsig,
@@ -251,7 +341,7 @@ def execute_multi(plans, x: np.ndarray, out_kind: str = 'cwt', shard: str = 'sig
     nsig = int(np.prod(lead)) if lead else 1
     nf = sum(p.nfreq for p in plans) if shard == 'scales' else p0.nfreq
     shape = (nf, p0.n) if out_kind in REDUCTIONS else lead + (nf, p0.n)
-    out = np.empty(shape, dtype=out_dtype(p0.dtype, out_kind))
+    out = HOST_POOL.empty(shape, out_dtype(p0.dtype, out_kind))
     arr = (ctypes.c_void_p * len(plans))(*[p.handle.value for p in plans])
     fn = L.lib().nw_execute_multi_scales if shard == 'scales' else L.lib().nw_execute_multi
     L.check(fn(arr, len(plans), x.ctypes.data_as(ctypes.c_void_p), nsig,

@@ -78,3 +78,58 @@ def test_default_line_carries_c3_and_c5_legs():
         assert c5['end_to_end_min_traffic']['bytes_per_step'] == pytest.approx(
             ((1 << 23) + 1) * 2 * esz + 512 * (1 << 24) * 2 * esz)
         assert c5['valu_roofline']['peak'] == peak
+
+
+def test_rccl_single_rank_bench_path():
+    """The driver's N-GPU launch (torchrun, one rank per GPU, backend nccl = RCCL) at N = 1 on
+    the lease: process group over RCCL, barriers, the device all_reduce(MAX) of the elapsed
+    time, real kernels (the sharded loop is mneutils.py:39's per-epoch batching)."""
+    from test_dist_cpu import free_port
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK')}
+    r = subprocess.run([sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '1',
+                        '--master-addr', '127.0.0.1', '--master-port', str(free_port()),
+                        os.path.join(ROOT, 'bench.py'), '--config', 'c3', '--epochs', '4', '--steps', '2',
+                        '--warmup', '1', '--backend', 'nccl', '--no-cpu-baseline'],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    d = json.loads(lines[0])
+    assert d['config']['process_group'] == 'nccl' and d['n_gpus'] == 1
+    assert d['value'] > 0 and d['roofline']['kernel'] == 'nw_fused_pair_kernel'
+
+
+def _nccl_worker(rank, world, port, out_dir):
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    import ninwavelets_amd as nw
+    from ninwavelets_amd import dist as D
+    os.environ['MASTER_ADDR'] = '127.0.0.1'
+    os.environ['MASTER_PORT'] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device('cuda', 0))
+    try:
+        rng = np.random.default_rng(11)
+        x = rng.standard_normal((7, 2048))
+        freqs = [3., 9., 27., 81.]
+        p = D.epochs_reduce(nw.Morse(1000), x, freqs, 'power_mean')
+        local = nw.Morse(1000).cwt(x[0], freqs)              # one rank: its slice is every scale
+        g = D.gather_scales(local, 4, device=torch.device('cuda', 0))
+        np.savez(os.path.join(out_dir, 'nccl.npz'), power=p, gathered=g, local=local, x=x)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_device_collectives_of_dist(tmp_path):
+    """dist.epochs_reduce's device all_reduce and gather_scales' all_gather through RCCL (one
+    rank on the lease's GPU: RCCL takes one GPU per rank), against the oracle."""
+    import numpy as np
+    import torch.multiprocessing as mp
+    from oracle import nw_oracle as O
+    from test_dist_cpu import free_port
+    mp.spawn(_nccl_worker, args=(1, free_port(), str(tmp_path)), nprocs=1, join=True)
+    got = np.load(tmp_path / 'nccl.npz')
+    c = O.epochs_cwt('morse', got['x'], [3., 9., 27., 81.])
+    ref = np.mean(np.abs(c) ** 2, axis=0)
+    assert np.max(np.abs(got['power'] - ref)) <= 1e-12 * np.max(ref)
+    np.testing.assert_array_equal(got['gathered'], got['local'])

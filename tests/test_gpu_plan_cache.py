@@ -48,3 +48,31 @@ def test_default_cap_keeps_plans_of_a_session():
     for S in (1, 4, 16):
         w.cwt_batch(synth(S, 2048, S).astype(np.float64), freqs)
     assert len(w._plans) == 3 and w.plan_cache_device_bytes() <= w.plan_cache_bytes
+
+
+def test_pooled_host_results_are_independent_arrays():
+    """Large host results come from the page-locked pool (engine.HOST_POOL, written by DMA
+    directly): each call still returns its own array, as the reference's new array per call
+    (base.py:378-407), equal to a result written into a caller-provided pageable array."""
+    import gc
+    from ninwavelets_amd import engine
+    freqs = np.arange(1, 65, dtype=np.float64)
+    w = nw.Morse(1000, dtype='float32')
+    x1, x2 = synth(64, 4096, 1), synth(64, 4096, 2)        # 64 x 64 x 4096 complex64 = 128 MiB
+    a = w.cwt_batch(x1, freqs)
+    b = w.cwt_batch(x2, freqs)
+    assert a.nbytes >= engine.HOST_POOL.min_bytes
+    assert engine.HOST_POOL.held >= a.nbytes + b.nbytes   # both page-locked, both alive
+    assert a.ctypes.data != b.ctypes.data
+    plan = next(iter(w._plans.values()))
+    ref = np.empty_like(a)                                  # pageable: the staged copy-out
+    plan.execute(x1, out=ref)
+    np.testing.assert_array_equal(a, ref)
+    plan.execute(x2, out=ref)
+    np.testing.assert_array_equal(b, ref)
+    pa = a.ctypes.data
+    del a
+    gc.collect()
+    c = w.cwt_batch(x2, freqs)                              # reuses the dropped buffer
+    assert c.ctypes.data == pa
+    np.testing.assert_array_equal(c, b)

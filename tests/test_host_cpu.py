@@ -239,3 +239,41 @@ def test_plugin_rows_are_the_references(name):
     np.testing.assert_array_equal(rows[0], g['w_first'])
     np.testing.assert_array_equal(rows[-1], g['w_last'])
     assert w._cache.kind == 'table'           # plugins take the host-table path
+
+
+def test_host_pool_recycles_and_caps():
+    """engine.HostPool (page-locked result arrays) with stand-in allocators, no GPU: a dropped
+    result's buffer serves the next result of its size; results the caller keeps are never
+    shared; past the cap results fall back to ordinary arrays; small results never pool."""
+    import gc
+    from ninwavelets_amd.engine import HostPool
+    store, freed = {}, []
+
+    def alloc(nb):
+        b = np.zeros(nb, dtype=np.uint8)
+        store[b.ctypes.data] = b
+        return b.ctypes.data
+
+    pool = HostPool(cap=3 * 4096, min_bytes=1024, keep_free=1, alloc=alloc, free=freed.append)
+    a = pool.empty((64, 8), np.float64)                  # 4096 B: pooled
+    assert a.ctypes.data in store and pool.held == 4096
+    a[:] = 1.0
+    b = pool.empty((64, 8), np.float64)
+    assert b.ctypes.data != a.ctypes.data                # both alive: distinct buffers
+    pa = a.ctypes.data
+    v = a[3:]                                           # a view keeps the buffer
+    del a
+    gc.collect()
+    c = pool.empty((512,), np.float64)
+    assert c.ctypes.data != pa
+    del v
+    gc.collect()
+    d = pool.empty((8, 64), np.float64)                  # same size: the released buffer
+    assert d.ctypes.data == pa and pool.held == 3 * 4096
+    e = pool.empty((64, 8), np.float64)                  # over the cap: an ordinary array
+    assert e.ctypes.data not in store and e.shape == (64, 8)
+    s = pool.empty((10,), np.float64)                    # below min_bytes
+    assert s.ctypes.data not in store
+    del b, c, d
+    gc.collect()
+    assert len(freed) == 2 and pool.free_bytes() == 4096  # keep_free = 1 per size
