@@ -105,6 +105,10 @@ __global__ __launch_bounds__(256) void kmax_kernel(WDesc d, int* __restrict__ km
 // here equals the nw_fused W table bit for bit -- but on 32-bit bin indices (n <= 2^24)
 // and with the per-scale constants hoisted.  j = k - off is the cached row's bin.
 template <typename T, int KIND> struct RowW;
+// fp64 Morse rows with r = 3 and 2b an integer in [0, 128) (the default b = 17.5): a kernel
+// instantiation of its own (host dispatch, morse_fast_of), since the general log-domain form's
+// ocml constants beside it spill
+constexpr int kMorseFast = 100;
 template <int KIND> struct RowW<float, KIND> {
     float xs, b, c1, rr, cpi, sigma, kappa, scale;
     int off, lenv, jlim;
@@ -154,10 +158,48 @@ template <int KIND> struct RowW<float, KIND> {
 // it (0.937 -> 0.697 ms without it).  Morlet / Shannon: psi_f64's expression.  (x^b and x^r by
 // repeated squaring measured slower: 76 B of scratch; x^3 as x*x*x for r = 3 spills 44-64 B:
 // the exp / log polynomial constants of ocml sit in ~22 VGPRs hoisted out of the row loop.)
+// exp(y) in fp64 (|error| < 1 ulp + the final scaling's rounding): y = k ln2 + r by Cody-Waite,
+// |r| <= ln2 / 2, 2^k * (Taylor polynomial of degree 13: truncation < 5e-18).  Written out
+// here so its constants are plain operands the compiler can keep in SGPRs (ocml's exp keeps
+// ~22 VGPRs of constants hoisted out of the row loop, which spilled every cheaper Morse form)
+// a constant materialised in an SGPR pair at its use (the empty volatile asm is neither
+// hoisted out of the row loop nor moved to VGPRs: one s_mov pair on the scalar unit per use)
+__device__ __forceinline__ double sconst(double c) {
+    asm volatile("" : "+s"(c));
+    return c;
+}
+__device__ __forceinline__ double exp_rows(double y) {
+    const double yc = fmin(fmax(y, -1100.0), 1100.0);      // k fits an int; NaN -> bound, fixed below
+    const double k = __builtin_rint(yc * sconst(1.4426950408889634074));
+    double rr = fma(-k, sconst(6.93147180369123816490e-01), yc);
+    rr = fma(-k, sconst(1.90821492927058770002e-10), rr);
+    double p = sconst(1.0 / 6227020800.0);                   // 1/13!
+    p = fma(p, rr, sconst(1.0 / 479001600.0));
+    p = fma(p, rr, sconst(1.0 / 39916800.0));
+    p = fma(p, rr, sconst(1.0 / 3628800.0));
+    p = fma(p, rr, sconst(1.0 / 362880.0));
+    p = fma(p, rr, sconst(1.0 / 40320.0));
+    p = fma(p, rr, sconst(1.0 / 5040.0));
+    p = fma(p, rr, sconst(1.0 / 720.0));
+    p = fma(p, rr, sconst(1.0 / 120.0));
+    p = fma(p, rr, sconst(1.0 / 24.0));
+    p = fma(p, rr, sconst(1.0 / 6.0));
+    p = fma(p, rr, 0.5);
+    p = fma(p, rr, 1.0);
+    p = fma(p, rr, 1.0);
+    const double e = ldexp(p, (int)k);
+    return y == y ? e : y;
+}
+
 template <int KIND> struct RowW<double, KIND> {
-    static constexpr bool MORSE = KIND == NW_MORSE;
+    static constexpr bool MORSE = KIND == NW_MORSE || KIND == kMorseFast;
+    // kMorseFast: x^b by a multiply chain (+ one sqrt for the half) and x^3 by two multiplies,
+    // then ONE exp -- 2 x^b exp((b/r)(1 - x^3)), the reference's own factorisation
+    // (wavelets.py:65-74) -- instead of one log and two exps
+    static constexpr bool FAST = KIND == kMorseFast;
     double delta, f, xs, peak, b, r, bor, sigma, cpi, kappa, scale;
     int off, lenv;
+    int bint, bhalf;
     __device__ static __forceinline__ double pin(double v) {
         const long long u = __double_as_longlong(v);
         const int lo = __builtin_amdgcn_readfirstlane((int)(u & 0xffffffffLL));
@@ -178,6 +220,8 @@ template <int KIND> struct RowW<double, KIND> {
         scale = d.scale;
         off = (int)d.off;
         lenv = d.len_valid < 0x7fffffff ? (int)d.len_valid : 0x7fffffff;
+        bint = FAST ? (int)(2.0 * d.b) / 2 : 0;
+        bhalf = FAST ? (int)(2.0 * d.b) & 1 : 0;
     }
     __device__ __forceinline__ double operator()(int j) const {
         if ((unsigned)j >= (unsigned)lenv) return 0.0;
@@ -185,8 +229,17 @@ template <int KIND> struct RowW<double, KIND> {
         if constexpr (MORSE) {
             const double x = (double)j * xs;
             if (!(x > 0.0)) return 0.0;
-            const double lx = log(x);
-            psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
+            if constexpr (FAST) {
+                double xb = bhalf ? sqrt(x) : 1.0, pw = x;
+                for (int e = bint; e; e >>= 1) {                 // uniform trip count
+                    if (e & 1) xb *= pw;
+                    pw *= pw;
+                }
+                psi = 2.0 * (xb * exp_rows(bor * (1.0 - x * x * x)));
+            } else {
+                const double lx = log(x);
+                psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
+            }
         } else if constexpr (KIND == NW_MORLET) {
             const double nu = (double)(int64_t)j * delta;
             const double x = nu / f * peak;
@@ -298,6 +351,9 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
                         const T w = wf(j);
 #endif
                         v[r] = C2<T>{w * xv.re, w * xv.im};
+                        // fp64 W: at most 4 evaluations in flight (they hold ~12 VGPRs each)
+                        if constexpr (sizeof(T) == 8 && (KIND == NW_MORSE || KIND == kMorseFast))
+                            if (r % 4 == 3) __builtin_amdgcn_sched_barrier(0);
                     }
                 } else {
                     v[r] = C2<T>{T(0), T(0)};
@@ -648,6 +704,15 @@ hipError_t large_transpose(const WDesc& d, int dtype, const void* X, void* scrat
 }
 
 namespace {
+// the fp64 row pass's fast Morse form applies (RowW<double, kMorseFast>)
+#ifndef NW_ROWS_MORSE_FAST
+#define NW_ROWS_MORSE_FAST 1
+#endif
+bool morse_fast_of(const WDesc& d) {
+    const double b2 = 2.0 * d.b;
+    return NW_ROWS_MORSE_FAST && d.kind == NW_MORSE && d.r == 3.0 && b2 >= 0.0 && b2 < 128.0 && b2 == (double)(int)b2;
+}
+
 template <typename T>
 hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, hipStream_t s) {
     const Split sp = split_of(d.n, sizeof(T) == 4 ? NW_F32 : NW_F64);
@@ -658,7 +723,10 @@ hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, 
         if constexpr (NN <= kMaxN2<T>) {                                                                     \
             constexpr int EE = kRowE<T, NN>;                                                                 \
             switch (d.kind) {                                                                                \
-                case NW_MORSE: return launch_row_pass<T, NN, EE, NW_MORSE>(d, f0, nf, sp.n1, Xt, B, km, s);     \
+                case NW_MORSE:                                                                               \
+                    if constexpr (sizeof(T) == 8)                                                            \
+                        if (morse_fast_of(d)) return launch_row_pass<T, NN, EE, kMorseFast>(d, f0, nf, sp.n1, Xt, B, km, s); \
+                    return launch_row_pass<T, NN, EE, NW_MORSE>(d, f0, nf, sp.n1, Xt, B, km, s);             \
                 case NW_MORLET: return launch_row_pass<T, NN, EE, NW_MORLET>(d, f0, nf, sp.n1, Xt, B, km, s);   \
                 case NW_SHANNON: return launch_row_pass<T, NN, EE, NW_SHANNON>(d, f0, nf, sp.n1, Xt, B, km, s); \
                 case NW_TABLE: return launch_row_pass<T, NN, kRowETab<T, NN>, NW_TABLE>(d, f0, nf, sp.n1, Xt, B, km, s); \

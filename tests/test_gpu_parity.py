@@ -324,12 +324,16 @@ def test_epochs_wavelet_power_matches_per_epoch_reference():
 # ------------------------------------------------------------------ C5 scale (N = 2^24)
 @pytest.mark.parametrize('kind,dtype', [('morse', 'float32'), ('shannon', 'float64'), ('morse', 'float64')])
 def test_c5_scale_single_signal(kind, dtype):
-    """One 2^24-sample signal (the rocFFT engine) at three of C5's 512 scales against
-    the fp64 oracle.  Tolerance at this length: 1e-4 (fp32), 1e-12 (fp64)."""
+    """One 2^24-sample signal at three of C5's 512 scales against the fp64 oracle, on the
+    auto engine: the two-pass form (nw_large.hip; Shannon's one distinct row through it and
+    k_expand_rows).  Tolerance at this length: 1e-4 (fp32), 1e-12 (fp64)."""
     n = 1 << 24
     freqs = np.linspace(0.5, 250, 512)[[0, 200, 511]]
     x = synth(1, n, 3)[0].astype(dtype)
-    out = CLASSES[kind](1000, dtype=dtype).cwt(x, freqs)
+    w = CLASSES[kind](1000, dtype=dtype)
+    out = w.cwt(x, freqs)
+    st = next(iter(w._plans.values())).stats()
+    assert st['engine'] == 'fused' and st['launches_rows'] > 0
     ref = O.cwt(kind, x.astype(np.float64), freqs)
     assert out.shape == (3, n)
     assert rel_err(out, ref) <= (1e-4 if dtype == 'float32' else 1e-12), rel_err(out, ref)
