@@ -701,11 +701,10 @@ template <typename T> __device__ __forceinline__ int dma_rounds_for(int nz) {
 // Measured (one box, interleaved): fp64 N = 4096 1.950 -> 1.900 ms per launch (+2.7 %), but
 // N = 16384 (E = 32, X by LDS-DMA) 9.80 -> 10.0-10.3 ms and the C5 fp64 row pass 0.94 -> 0.95:
 // on for N <= 4096 only.
-// FORCE: on at any N (the fp64 one-pass kernels whose next-signal loads are all issued before
-// the stores, nw_fused.hip kTwfOf: a twiddle base loaded from the global table after the stores
-// would wait for all of them)
-template <typename T, int N, int E, bool FORCE = false> struct TwSplit {
-    static constexpr bool ON = std::is_same<T, double>::value && ((N >= 2048 && N <= 4096) || FORCE);
+// (At N = 16384 measured again in round 4, beside the next signal's W loaded before the
+// stores and alone: +-0 / slower, profiles/r04_ab_fused.txt.)
+template <typename T, int N, int E> struct TwSplit {
+    static constexpr bool ON = std::is_same<T, double>::value && N >= 2048 && N <= 4096;
     static constexpr int NHI = N / 64, COUNT = NHI + 32;
     static constexpr int OFFSET = kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES;
     static_assert(OFFSET % 16 == 0, "table alignment");
@@ -721,13 +720,8 @@ template <typename T, int N, int E, bool FORCE = false> struct TwSplit {
         }
     }
 };
-template <typename T, int N, int E, bool TWF = false> constexpr int kLdsBytes =
-    kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES + TwSplit<T, N, E, TWF>::BYTES;
-
-// no-op hook of passes_from (see PF there)
-struct NoPrefetch {
-    __device__ __forceinline__ void operator()() const {}
-};
+template <typename T, int N, int E> constexpr int kLdsBytes =
+    kImgElems<T, N, E> * (int)sizeof(T) + Tab1<T, N, E>::BYTES + TwSplit<T, N, E>::BYTES;
 
 
 // ---- exchange pass P-1 -> P through the half image (re, then im), then compute pass P.
@@ -739,16 +733,11 @@ struct NoPrefetch {
 // T = f2 (signal pairs): every element carries two signals' values; twiddles and the Tab1
 // table stay scalar (shared), and the last pass stores the low halves to ocur and the high
 // halves to ocur2 (nullptr: an odd last signal, its high half is not stored).
-//
-// TWF: twiddle bases from the LDS split table (TwSplit<..., TWF>) at any N.  PF: called once in
-// the last pass after its arithmetic and before this signal's stores, when a next signal
-// exists (the caller's loads for the next signal, so they do not queue behind the stores).
-template <typename T, int N, int E, int OUT, int P, bool XD, int SP = kStoreGlobal, bool TWF = false,
-          typename PF = NoPrefetch>
+template <typename T, int N, int E, int OUT, int P, bool XD, int SP = kStoreGlobal>
 __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc<T>>* __restrict__ tw, C2<T>* x,
                                             const C2<T>* xs_next, void* ocur,
                                             Stamps* st, void* ocur2 = nullptr, int dma_rounds = 1 << 30,
-                                            double* acc = nullptr, const void* xs_next2 = nullptr, PF pf = PF{}) {
+                                            double* acc = nullptr, const void* xs_next2 = nullptr) {
     using S = Sc<T>;
     constexpr bool PAIRSIG = !std::is_same<T, S>::value;
     constexpr int OSZ = (int)sizeof(typename OutT<OUT, S>::type);
@@ -756,9 +745,9 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
     if constexpr (P < Geometry<N, E>::npass()) {
         constexpr int R = I::R, Q = I::Q, LR = ilog2<R>();
         constexpr bool TABLED = P == 1 && Tab1<T, N, E>::ON;
-        constexpr bool SPLIT = TwSplit<T, N, E, TWF>::ON;
+        constexpr bool SPLIT = TwSplit<T, N, E>::ON;
         const C2<S>* split = nullptr;
-        if constexpr (SPLIT) split = reinterpret_cast<const C2<S>*>(TwSplit<T, N, E, TWF>::table(lds));
+        if constexpr (SPLIT) split = reinterpret_cast<const C2<S>*>(TwSplit<T, N, E>::table(lds));
         C2<S> pb[Q][LR > 0 ? LR : 1];
 #ifndef NW_ABL_NOTWIDDLE
         if constexpr (!TABLED && I::PAIRED && Q == 2) {
@@ -904,15 +893,6 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                 }
         } else if constexpr (I::LAST) {
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (XD && !std::is_same<PF, NoPrefetch>::value) {
-                // after the arithmetic (the twiddles are dead: only the outputs and the
-                // prefetched values are live), before the stores.  The empty asm reads every
-                // output and clobbers memory, so the loads cannot be hoisted above the arithmetic
-#pragma unroll
-                for (int e = 0; e < E; ++e) asm volatile("" ::"v"(v[e].re), "v"(v[e].im) : "memory");
-                if (xs_next) pf();
-                __builtin_amdgcn_sched_barrier(0);
-            }
             if constexpr (PAIRSIG) {
                 C2<S> a[E], b[E];
 #pragma unroll
@@ -926,8 +906,7 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                 LastStores<T, N, E, OUT, SP>::all(v, ocur, t);
             }
         } else {
-            passes_from<T, N, E, OUT, P + 1, XD, SP, TWF, PF>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, acc,
-                                                             xs_next2, pf);
+            passes_from<T, N, E, OUT, P + 1, XD, SP>(v, lds, t, tw, x, xs_next, ocur, st, ocur2, dma_rounds, acc, xs_next2);
         }
     }
 }

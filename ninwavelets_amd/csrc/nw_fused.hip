@@ -97,35 +97,14 @@ template <typename T> constexpr int kTileGT = kTileG;
 // registers per element); the partial-sum kernels hold fp64 accumulators on top: ITC (2E) at 3 waves/SIMD,
 // power at E = 32 at 2
 constexpr int kWpsF32 = 4, kWpsF64 = 2, kWpsPhSum = 3, kWpsPSum32 = 2;
-// fp64 kernels with X by LDS-DMA (E = 32, n = 8192 / 16384): one block per CU at n = 16384, so
-// nothing but the block itself overlaps its store burst -- and a vector load issued after the
-// stores waits for all of them (in-order vmcnt).  WPF: the next signal's W elements are loaded
-// into registers before the current signal's stores (passes_from's PF hook); TWF: the twiddle
-// bases come from the LDS split table instead of the global table.  Together no vector load of
-// the next signal is issued behind the stores.
-#ifndef NW_F64_PF
-#define NW_F64_PF 0
-#endif
-#ifndef NW_F64_TWL
-#define NW_F64_TWL 0
-#endif
-// elements of W prefetched (the rest is loaded in pass 0)
-#ifndef NW_F64_PFN
-#define NW_F64_PFN 32
-#endif
-constexpr int kWpfN = NW_F64_PFN;
-// the second half of a block's waves at s_setprio 1 (MI355X_MICROARCH.md "Two waves per SIMD"
-// item 4: the younger half loses every arbitration at equal priority)
-#ifndef NW_SETPRIO
-#define NW_SETPRIO 0
-#endif
+// fp64 one-pass kernels (E = 32, X by LDS-DMA): the second half of a block's waves at s_setprio 1 (MI355X_MICROARCH.md
+// "Two waves per SIMD", item 4: at equal priority the younger half loses every arbitration).
+// fp64 C4 shape 7.92-7.99 -> 7.89-7.90 ms per launch; fp32 C4 +-0, C3 (signal pairs) +10 %:
+// fp64 only (tools/ab.sh, profiles/r04_ab_fused.txt)
+template <typename T> constexpr bool kPrioHalf = sizeof(T) == 8;
 __device__ __forceinline__ void prio_half(int t, int threads) {
-    if constexpr (NW_SETPRIO) {
-        if (__builtin_amdgcn_readfirstlane(t) >= threads / 2) __builtin_amdgcn_s_setprio(1);
-    }
+    if (__builtin_amdgcn_readfirstlane(t) >= threads / 2) __builtin_amdgcn_s_setprio(1);
 }
-template <typename T, int E, bool REALW> constexpr bool kWpfOf = NW_F64_PF && sizeof(T) == 8 && kXDMA<T, E, REALW>;
-template <typename T, int E, bool REALW> constexpr bool kTwfOf = NW_F64_TWL && sizeof(T) == 8 && kXDMA<T, E, REALW>;
 template <typename T, int E, int OUT>
 constexpr int kWpsOf = sizeof(T) == 8 ? kWpsF64 : OUT == kOutPhSum ? kWpsPhSum
                      : (OUT == kOutPSum && E >= 32) ? kWpsPSum32 : kWpsF32;
@@ -141,7 +120,6 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     using G = Geometry<N, E>;
     using WT = typename WLoad<T, REALW>::type;
     constexpr bool XD = kXDMA<T, E, REALW>;
-    constexpr bool PSUMK = OUT == kOutPSum || OUT == kOutPhSum;
     // the LDS-DMA copies dma_rounds_for(nzv) rounds of the bins pass-0 variant nzv reads; with a
     // shifted support table (WSH > 0: nz = wnz >> WSH can be 6 or 10, between the variants) it
     // would copy fewer bins than the dispatched variant reads.  The shift only occurs for the
@@ -150,7 +128,7 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     extern __shared__ __align__(16) unsigned char smem[];
     T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
-    prio_half(t, N / E);
+    if constexpr (kPrioHalf<T> && XD) prio_half(t, N / E);   // the measured case: E = 32 output kernels
 
     // XCD-aware block -> (scale, signal group).  Blocks b, b+8, b+16, ... share an XCD
     // (and its 4 MiB L2); the ~64 of them resident at a time cover a tile of
@@ -176,8 +154,6 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     const WT* wrow = reinterpret_cast<const WT*>(wtab) + (int64_t)fi * N;
     const uint32_t wo = (uint32_t)t * (uint32_t)sizeof(WT);
     constexpr bool WREG = E <= kWregMaxE && !(sizeof(T) == 8 && N / E > 512);
-    constexpr bool WPF = kWpfOf<T, E, REALW> && !PSUMK;
-    constexpr bool TWF = kTwfOf<T, E, REALW> && !PSUMK;
     WT w[WREG ? E : 1];
     if constexpr (WREG) {
 #pragma unroll
@@ -192,12 +168,8 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
 #pragma unroll
         for (int r = 0; r < WKEEP; ++r) wk[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
     }
-    // WPF: W of the signal being transformed, reloaded for the next one before the stores
-    constexpr int NPF = WPF ? (kWpfN < E ? kWpfN : E) : 0;
-    WT wn[NPF > 0 ? NPF : 1];
     auto w_at = [&](int r) -> WT {
         if constexpr (WREG) return w[r];
-        else if (r < NPF) return wn[r < NPF ? r : 0];
         else if (r < WKEEP) return wk[r < WKEEP ? r : 0];
 #ifdef NW_ABL_NOWLOAD   // diagnostic only (wrong results): W beyond WKEEP without its global loads
         else { WT z{}; if constexpr (REALW) z = (T)(r + 1); return z; }
@@ -214,8 +186,8 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     Stamps* st = nullptr;
 #endif
     Tab1<T, N, E>::fill(lds, tw, t);   // read after the first exchange's barriers
-    TwSplit<T, N, E, TWF>::fill(lds, tw, t);
-    if constexpr (TwSplit<T, N, E, TWF>::ON) lds_barrier();   // read before the first exchange
+    TwSplit<T, N, E>::fill(lds, tw, t);
+    if constexpr (TwSplit<T, N, E>::ON) lds_barrier();   // read before the first exchange
     C2<T> x[E];
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<T>) : sizeof(T));
     // XDMA: X[N/2] (the real Nyquist bin, outside the DMA'd half) of the signal being
@@ -238,17 +210,6 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     // i.e. NZ/2 rounds of 2*T bins, when it reads no mirrored bin (NZ <= E/2)
     const int nzv = nz < kPruneMin ? kPruneMin : nz;
     const int dma_rounds = nzv <= E / 2 ? dma_rounds_for<T>(nzv) : 1 << 30;
-    // WPF: the W elements the dispatched pass-0 variant reads (fp64 variants 4, 8, 16, 24, E)
-    const int nzw = nz <= 4 ? 4 : nz <= 8 ? 8 : nz <= 16 ? 16 : (kNz24Of<T, N, E> && nz <= 24) ? 24 : E;
-    auto load_w = [&]() {
-        if constexpr (WPF) {
-            // every element (a uniform branch per element put wn in scratch); those past the
-            // row's support are exact zeros from L2 that the dispatched variant never reads
-#pragma unroll
-            for (int r = 0; r < NPF; ++r) wn[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(WT)));
-        }
-    };
-    load_w();
     // power partial sums (kOutPSum): sum over the block's signals of |y|^2 per output point
     // (kOutPhSum: the sums of y / |y|, two fp64 values per point)
     constexpr bool PSUM = OUT == kOutPSum || OUT == kOutPhSum;
@@ -289,24 +250,13 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
                         if (r == E / 2 && t == 0) x[r] = nyq;   // lvalue select (nyq -> scratch)
                         x[r].im = -x[r].im;
                     }
-                    if constexpr (WPF) {
-                        // multiply as X arrives, at most 8 reads in flight (all 32 complex X at
-                        // once beside W and v exceed 256 VGPRs)
-                        v[r] = WLoad<T, REALW>::apply(w_at(r), x[r]);
-                        if (r % 8 == 7) __builtin_amdgcn_sched_barrier(0);
-                    }
                 }
             } else {
                 load_x<T, N, E, NZ>(x, reinterpret_cast<const C2<T>*>(X + s * d.nh), t);
             }
 #pragma unroll
-            for (int r = 0; r < E; ++r) {
-                if constexpr (WPF && XD) {
-                    if (r >= NZ) v[r] = C2<T>{T(0), T(0)};
-                } else {
-                    v[r] = r < NZ ? WLoad<T, REALW>::apply(w_at(r), x[r]) : C2<T>{T(0), T(0)};
-                }
-            }
+            for (int r = 0; r < E; ++r)
+                v[r] = r < NZ ? WLoad<T, REALW>::apply(w_at(r), x[r]) : C2<T>{T(0), T(0)};
             idft_br<T, E, NZ>(v);
         };
         if (nz <= 4) pass0.template operator()<4>();
@@ -322,8 +272,8 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
         NW_STAMP(st, 0);                       // pass 0: X wait + radix-E arithmetic
         const C2<T>* xs_next = s + 1 < s_end ? reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) : nullptr;
         void* ocur = (char*)out + (s * d.nfreq + fi) * (int64_t)N * out_esz;   // row of signal s
-        passes_from<T, N, E, OUT, 1, XD, (sizeof(T) == 8 ? kStoreGlobalNt : kStoreGlobal), TWF>(
-            v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds, PSUM ? acc : nullptr, nullptr, load_w);
+        passes_from<T, N, E, OUT, 1, XD, (sizeof(T) == 8 ? kStoreGlobalNt : kStoreGlobal)>(
+            v, lds, t, tw, x, xs_next, ocur, st, nullptr, dma_rounds, PSUM ? acc : nullptr);
     }
     if constexpr (PSUM) {
         // the block's partial: row (group sg, scale fi) of the (groups, F, N) partial buffer
@@ -369,7 +319,6 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
     extern __shared__ __align__(16) unsigned char smem[];
     f2* lds = reinterpret_cast<f2*>(smem);
     const int t = threadIdx.x;
-    prio_half(t, N / E);
     // XCD-aware block -> (scale, signal group): as nw_fused_kernel
     const int b = blockIdx.x;
     const int xcd = b & 7;
@@ -652,7 +601,7 @@ template <typename T, int N, int E, bool REALW>
 hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
                     hipStream_t s) {
     constexpr int threads = N / E;
-    const size_t lds = (size_t)kLdsBytes<T, N, E, kTwfOf<T, E, REALW>>;
+    const size_t lds = (size_t)kLdsBytes<T, N, E>;
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
@@ -737,7 +686,7 @@ hipError_t prepare_one() {
                                     hipFuncAttributeMaxDynamicSharedMemorySize, lp);
         if (e != hipSuccess) return e;
     }
-    const int lds = kLdsBytes<T, N, E, kTwfOf<T, E, REALW>>;
+    const int lds = kLdsBytes<T, N, E>;
     hipError_t e = hipFuncSetAttribute((const void*)nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e == hipSuccess)

@@ -53,7 +53,11 @@ constexpr int kRowTileG = 8;      // row groups per XCD tile
 // 1.039 -> 0.978 ms per launch against 512 threads)
 // cols_kernel workgroup size (C * N1 / E)
 template <typename T> constexpr int kColThreads = 1024;
-constexpr size_t kBBudget = size_t(2) << 30;   // bytes of B per launch pair (scales chunked to fit)
+// bytes of B per launch pair (scales chunked to fit): 8 GiB = 64 scales of fp32 / 32 of fp64 at
+// C5.  Against 2 GiB (16 / 8 scales): C5 fp32 47.49 -> 46.15 ms per step, fp64 118.19 -> 113.15
+// (fewer, longer launches: the row pass's XCD tiles of 8 scales fill, fewer tails;
+// profiles/r04_c5_fchunk.txt)
+constexpr size_t kBBudget = size_t(8) << 30;
 
 // N2 (on-chip rows) and its elements per thread E: the nw_fused sizes (fp64: E = 16, N2 <= 8192)
 template <typename T, int N2> constexpr int kRowE = N2 >= 8192 ? 32 : 16;
@@ -257,6 +261,8 @@ template <int KIND> struct RowW<double, KIND> {
 // fp32 E = 32 rows: pruned Xt rows by LDS-DMA ahead of the stores (C5 50.6 -> 48.5 ms per step);
 // analytic kinds only (table rows' wavelet_bin loads would exceed 128 VGPRs, as in nw_fused);
 // fp64 rows with the same DMA measured no faster (0.94 -> 0.98 ms per launch)
+// (fp64 rows with the DMA, re-measured in round 4 beside the fast Morse form: no gain either,
+// profiles/r04_c5f64_rows_ab.txt)
 template <typename T, int E, int KIND>
 constexpr bool kRowsXD = sizeof(T) == 4 && E >= 32 && KIND != NW_TABLE;
 // 4 waves/SIMD; fp64: 2 (twice the registers per element, as nw_fused)
@@ -705,12 +711,9 @@ hipError_t large_transpose(const WDesc& d, int dtype, const void* X, void* scrat
 
 namespace {
 // the fp64 row pass's fast Morse form applies (RowW<double, kMorseFast>)
-#ifndef NW_ROWS_MORSE_FAST
-#define NW_ROWS_MORSE_FAST 1
-#endif
 bool morse_fast_of(const WDesc& d) {
     const double b2 = 2.0 * d.b;
-    return NW_ROWS_MORSE_FAST && d.kind == NW_MORSE && d.r == 3.0 && b2 >= 0.0 && b2 < 128.0 && b2 == (double)(int)b2;
+    return d.kind == NW_MORSE && d.r == 3.0 && b2 >= 0.0 && b2 < 128.0 && b2 == (double)(int)b2;
 }
 
 template <typename T>

@@ -183,3 +183,20 @@ def test_fused_fp64_16384_one_pass(kind, out):
         ref = O.cwt(kind, x[s], freqs)
         ref = {'cwt': ref, 'power': np.abs(ref) ** 2, 'abs': np.abs(ref)}[out]
         assert rel_err(got[s], ref) <= (2e-12 if out == 'power' else 1e-12), (s, rel_err(got[s], ref))
+
+
+@pytest.mark.parametrize('dtype', ['float32', 'float64'])
+def test_large_scale_chunks_are_exact(dtype, monkeypatch):
+    """The two-pass form runs its scales in chunks sized to the B budget (8 GiB: one chunk at
+    this length); chunks of 2 scales (NW_LARGE_FCHUNK, diagnostics) give the same bits."""
+    n = 1 << 15
+    x = synth(2, n, seed=21).astype(dtype)
+    freqs = np.array([1.0, 5.0, 17.0, 60.0, 140.0])
+    whole = nw.Morse(1000, dtype=dtype).cwt_batch(x, freqs)
+    monkeypatch.setenv('NW_LARGE_FCHUNK', '2')
+    w = nw.Morse(1000, dtype=dtype)
+    chunked = w.cwt_batch(x, freqs)
+    assert large_ran(w)
+    st = next(iter(w._plans.values())).stats()
+    assert st['launches_rows'] == 3                       # ceil(5 / 2) row-pass launches
+    np.testing.assert_array_equal(chunked, whole)
