@@ -28,8 +28,8 @@ for c in $CFGS; do
   case $c in
     c4) record c4 "--steps 10 --warmup 3" "--config c4 --steps 2 --warmup 1 --legs none" "nw_fused_kernel" '{"chunk": 512, "n": 16384, "freqs": 256, "out": "cwt", "dtype": "float32"}' || exit $? ;;
     c3) record c3 "--config c3 --steps 5 --warmup 2" "--config c3 --steps 2 --warmup 1" "nw_fused_pair_kernel" '{"chunk": 1024, "n": 4096, "freqs": 256, "out": "power", "dtype": "float32"}' || exit $? ;;
-    c5) record c5 "--config c5 --steps 3 --warmup 1" "--config c5 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float32", "scales_per_launch": 16}' || exit $? ;;
-    c5f64) record c5f64 "--config c5 --dtype float64 --steps 3 --warmup 1" "--config c5 --dtype float64 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float64", "scales_per_launch": 16}' || exit $? ;;
+    c5) record c5 "--config c5 --steps 3 --warmup 1" "--config c5 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float32", "scales_per_launch": 64}' || exit $? ;;
+    c5f64) record c5f64 "--config c5 --dtype float64 --steps 3 --warmup 1" "--config c5 --dtype float64 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float64", "scales_per_launch": 32}' || exit $? ;;
     c4f64) record c4f64 "--config c4 --dtype float64 --steps 3 --warmup 1" "--config c4 --dtype float64 --epochs 16 --steps 2 --warmup 1" "nw_fused_kernel" '{"chunk": 512, "n": 16384, "freqs": 256, "out": "cwt", "dtype": "float64"}' || exit $? ;;
   esac
 done
