@@ -198,5 +198,5 @@ def test_large_scale_chunks_are_exact(dtype, monkeypatch):
     chunked = w.cwt_batch(x, freqs)
     assert large_ran(w)
     st = next(iter(w._plans.values())).stats()
-    assert st['launches_rows'] == 3                       # ceil(5 / 2) row-pass launches
+    assert st['launches_rows'] == 2 * 3                   # per signal, ceil(5 / 2) row-pass launches
     np.testing.assert_array_equal(chunked, whole)
