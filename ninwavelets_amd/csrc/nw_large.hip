@@ -582,6 +582,137 @@ __global__ __launch_bounds__(kColThreads<T>, sizeof(T) == 8 ? 2 : 4) void cols_k
     col_passes<T, N1, N2, OUT, 0>(v, lds, u, c, orow, ooff, tw1);
 }
 
+// ---- fp32 column pass on column PAIRS: thread (cp, u) owns the adjacent columns 2cp, 2cp+1
+// and E2 = 16 elements k1 = u + U2 r of each, every lane value a C2<f2> holding the two columns
+// (signal-pair technique of nw_fused_pair_kernel): B is read and y written 16 B per lane
+// (two complex64) instead of 8, every butterfly / twiddle / LDS access serves both columns
+// (v_pk_* math, 8-B image slots [position][pair]), the same C = 2 CP columns per 1024-thread
+// workgroup and 256-B runs.  Length-N1 transforms at E = 16 take one exchange more than E = 32.
+template <int N1> struct ColsP {
+    static constexpr int E = 16;
+    static constexpr int U = N1 / E;                 // threads per column pair
+    static constexpr int CP = 1024 / U;              // column pairs per workgroup
+    static constexpr int C = 2 * CP;
+    using G = Geometry<N1, E>;
+    static_assert(N1 >= 32 && CP >= 16, "column-pair geometry");
+};
+
+template <int N1, int P, int COMP>
+__device__ __forceinline__ void colp_write(C2<f2>* v, f2* lds, int u, int cp) {
+    using CL = ColsP<N1>;
+    using G = typename CL::G;
+    constexpr int CP = CL::CP, U = CL::U;
+    constexpr int R = G::radix(P), NS = G::ns(P), Q = CL::E / R;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const int j = u + q * U;
+        f2* dst = lds + ((j / NS) * NS * R + j % NS) * CP + cp;
+#pragma unroll
+        for (int i = 0; i < R; ++i) dst[bitrev<R>(i) * NS * CP] = comp<COMP>(v[q * R + i]);
+    }
+}
+
+template <int N1, int P, int COMP>
+__device__ __forceinline__ void colp_read(C2<f2>* v, const f2* lds, int u, int cp) {
+    using CL = ColsP<N1>;
+    using G = typename CL::G;
+    constexpr int CP = CL::CP, U = CL::U;
+    constexpr int R = G::radix(P), Q = CL::E / R, STRIDE = N1 / R;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+        const f2* src = lds + (u + q * U) * CP + cp;
+#pragma unroll
+        for (int r = 0; r < R; ++r) comp<COMP>(v[q * R + r]) = src[r * STRIDE * CP];
+    }
+}
+
+template <int N1, int N2, int OUT, int P>
+__device__ __forceinline__ void colp_passes(C2<f2>* v, f2* lds, int u, int cp, void* orow, uint32_t lane_off) {
+    using CL = ColsP<N1>;
+    using G = typename CL::G;
+    constexpr int U = CL::U;
+    constexpr int R = G::radix(P), NS = G::ns(P), Q = CL::E / R;
+    if constexpr (P > 0) {
+        constexpr int LR = ilog2<R>();
+        lds_barrier();
+        colp_write<N1, P - 1, 0>(v, lds, u, cp);
+        lds_barrier();
+        colp_read<N1, P, 0>(v, lds, u, cp);
+        lds_barrier();
+        colp_write<N1, P - 1, 1>(v, lds, u, cp);
+        lds_barrier();
+        colp_read<N1, P, 1>(v, lds, u, cp);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            C2<float> pb[LR > 0 ? LR : 1];                  // shared by the two columns
+            twiddle_bases<float, R, N1, NS * R>(pb, (u + q * U) % NS, nullptr);
+            twiddle_apply<f2, R>(v + q * R, pb);
+            idft_br<f2, R>(v + q * R);
+        }
+    }
+    if constexpr (P + 1 < G::npass()) {
+        colp_passes<N1, N2, OUT, P + 1>(v, lds, u, cp, orow, lane_off);
+    } else {
+        // v[q*R + i] is y at n1 = u + q*U + bitrev(i)*NS (the last pass has NS butterflies)
+        using O = typename OutT<OUT, float>::type;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+#pragma unroll
+            for (int i = 0; i < R; ++i) {
+                const uint32_t cn1 = (uint32_t)(q * U + bitrev<R>(i) * NS);
+                const C2<f2> y = v[q * R + i];
+                O* dst = at(reinterpret_cast<O*>(orow), lane_off, cn1 * (uint32_t)N2 * (uint32_t)sizeof(O));
+                if constexpr (OUT == NW_OUT_CWT) {
+                    using V4 = float __attribute__((ext_vector_type(4)));
+                    __builtin_nontemporal_store(V4{y.re.x, y.im.x, y.re.y, y.im.y}, reinterpret_cast<V4*>(dst));
+                } else {
+                    const f2 o{out_value<OUT, float>(C2<float>{y.re.x, y.im.x}),
+                               out_value<OUT, float>(C2<float>{y.re.y, y.im.y})};
+                    __builtin_nontemporal_store(o, reinterpret_cast<f2*>(dst));
+                }
+            }
+        }
+    }
+}
+
+template <int N1, int N2, int OUT>
+__global__ __launch_bounds__(1024, 4) void cols_kernel(int f0, int nf, const C2<float>* __restrict__ B,
+                                                       void* __restrict__ out) {
+    using CL = ColsP<N1>;
+    constexpr int CP = CL::CP, C = CL::C, U = CL::U, E = CL::E;
+    constexpr int64_t n = (int64_t)N1 * N2;
+    extern __shared__ __align__(16) unsigned char smem[];
+    f2* lds = reinterpret_cast<f2*>(smem);
+    const int t = threadIdx.x;
+    const int cp = t % CP, u = t / CP;
+    constexpr int ngroups = N2 / C;
+    const int fl = blockIdx.x / ngroups;
+    const int cg = blockIdx.x % ngroups;
+    if (fl >= nf) return;
+    const int col = cg * C + 2 * cp;                 // n2 of the pair's first column
+    const C2<float>* bf = B + (int64_t)fl * n;
+    const uint32_t boff = ((uint32_t)u * N2 + (uint32_t)col) * (uint32_t)sizeof(C2<float>);
+    // pass 0: v[r] = B[k1][n2 .. n2+1] * w_n^(n2 k1), k1 = u + U r
+    C2<f2> v[E];
+#pragma unroll
+    for (int r = 0; r < E; ++r) {
+        const int k1 = u + U * r;
+        using V4 = float __attribute__((ext_vector_type(4)));
+        const V4 b4 = *reinterpret_cast<const V4*>(at(bf, boff, (uint32_t)(U * r * N2 * sizeof(C2<float>))));
+        const uint32_t m0 = (uint32_t)col * (uint32_t)k1;                 // n2 k1 < n <= 2^24
+        constexpr float inv_n = 1.0f / (float)n;                          // exact: power of two
+        const float r0 = (float)m0 * inv_n, r1 = (float)(m0 + (uint32_t)k1) * inv_n;
+        const C2<f2> w{f2{__builtin_amdgcn_cosf(r0), __builtin_amdgcn_cosf(r1)},
+                       f2{__builtin_amdgcn_sinf(r0), __builtin_amdgcn_sinf(r1)}};
+        v[r] = cmul(C2<f2>{f2{b4.x, b4.z}, f2{b4.y, b4.w}}, w);
+    }
+    idft_br<f2, E>(v);
+    using O = typename OutT<OUT, float>::type;
+    void* orow = reinterpret_cast<char*>(out) + (int64_t)(f0 + fl) * n * (int64_t)sizeof(O);
+    const uint32_t ooff = ((uint32_t)col + (uint32_t)u * N2) * (uint32_t)sizeof(O);
+    colp_passes<N1, N2, OUT, 0>(v, lds, u, cp, orow, ooff);
+}
+
 // tsplit for one n (fp64 column pass), from sincospi in fp64
 __global__ __launch_bounds__(256) void tsplit_kernel(C2<double>* ts, int64_t n) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -611,8 +742,28 @@ hipError_t launch_row_pass(const WDesc& d, int f0, int nf, int n1, const C2<T>* 
     return hipGetLastError();
 }
 
+#ifndef NW_COLS_PAIR
+#define NW_COLS_PAIR 1
+#endif
 template <typename T, int N1, int N2>
 hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, const C2<T>* tsplit, hipStream_t s) {
+    if constexpr (sizeof(T) == 4 && NW_COLS_PAIR && ColsP<N1>::CP >= 16 && N2 % ColsP<N1>::C == 0) {
+        using CL = ColsP<N1>;
+        const int lds = N1 * CL::C * (int)sizeof(float);
+        const int64_t blocks = (int64_t)nf * (N2 / CL::C);
+        const void* fn = out_kind == NW_OUT_CWT     ? (const void*)cols_kernel<N1, N2, NW_OUT_CWT>
+                         : out_kind == NW_OUT_POWER ? (const void*)cols_kernel<N1, N2, NW_OUT_POWER>
+                                                    : (const void*)cols_kernel<N1, N2, NW_OUT_ABS>;
+        hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+        if (e != hipSuccess) return e;
+        if (out_kind == NW_OUT_CWT)
+            cols_kernel<N1, N2, NW_OUT_CWT><<<(unsigned)blocks, 1024, lds, s>>>(f0, nf, B, out);
+        else if (out_kind == NW_OUT_POWER)
+            cols_kernel<N1, N2, NW_OUT_POWER><<<(unsigned)blocks, 1024, lds, s>>>(f0, nf, B, out);
+        else
+            cols_kernel<N1, N2, NW_OUT_ABS><<<(unsigned)blocks, 1024, lds, s>>>(f0, nf, B, out);
+        return hipGetLastError();
+    }
     using CL = Cols<T, N1>;
     const int lds = N1 * CL::C * (int)sizeof(T);
     const int64_t blocks = (int64_t)nf * (N2 / CL::C);
