@@ -588,10 +588,13 @@ __global__ __launch_bounds__(kColThreads<T>, sizeof(T) == 8 ? 2 : 4) void cols_k
 // (two complex64) instead of 8, every butterfly / twiddle / LDS access serves both columns
 // (v_pk_* math, 8-B image slots [position][pair]), the same C = 2 CP columns per 1024-thread
 // workgroup and 256-B runs.  Length-N1 transforms at E = 16 take one exchange more than E = 32.
+// (E = 32 with 512-thread workgroups: one exchange instead of two, 198 VGPRs at 2 waves/SIMD:
+// C5 cols 3.92 -> 3.95 ms per launch, not kept; profiles/r04_c5_colpairs_ab.txt)
 template <int N1> struct ColsP {
     static constexpr int E = 16;
+    static constexpr int THREADS = 1024;
     static constexpr int U = N1 / E;                 // threads per column pair
-    static constexpr int CP = 1024 / U;              // column pairs per workgroup
+    static constexpr int CP = THREADS / U;           // column pairs per workgroup
     static constexpr int C = 2 * CP;
     using G = Geometry<N1, E>;
     static_assert(N1 >= 32 && CP >= 16, "column-pair geometry");
@@ -676,7 +679,7 @@ __device__ __forceinline__ void colp_passes(C2<f2>* v, f2* lds, int u, int cp, v
 }
 
 template <int N1, int N2, int OUT>
-__global__ __launch_bounds__(1024, 4) void cols_kernel(int f0, int nf, const C2<float>* __restrict__ B,
+__global__ __launch_bounds__(ColsP<N1>::THREADS, ColsP<N1>::THREADS / 256) void cols_kernel(int f0, int nf, const C2<float>* __restrict__ B,
                                                        void* __restrict__ out) {
     using CL = ColsP<N1>;
     constexpr int CP = CL::CP, C = CL::C, U = CL::U, E = CL::E;
@@ -742,12 +745,12 @@ hipError_t launch_row_pass(const WDesc& d, int f0, int nf, int n1, const C2<T>* 
     return hipGetLastError();
 }
 
-#ifndef NW_COLS_PAIR
-#define NW_COLS_PAIR 1
-#endif
+// fp32: the column-pair kernel (C5 cols 4.02 -> 3.86 ms per 64-scale launch against the
+// single-column kernel, which fp64 keeps: its lanes already read and write 16 B)
+constexpr bool kColsPair = true;
 template <typename T, int N1, int N2>
 hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, const C2<T>* tsplit, hipStream_t s) {
-    if constexpr (sizeof(T) == 4 && NW_COLS_PAIR && ColsP<N1>::CP >= 16 && N2 % ColsP<N1>::C == 0) {
+    if constexpr (sizeof(T) == 4 && kColsPair && ColsP<N1>::CP >= 16 && N2 % ColsP<N1>::C == 0) {
         using CL = ColsP<N1>;
         const int lds = N1 * CL::C * (int)sizeof(float);
         const int64_t blocks = (int64_t)nf * (N2 / CL::C);
@@ -757,11 +760,11 @@ hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, 
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         if (out_kind == NW_OUT_CWT)
-            cols_kernel<N1, N2, NW_OUT_CWT><<<(unsigned)blocks, 1024, lds, s>>>(f0, nf, B, out);
+            cols_kernel<N1, N2, NW_OUT_CWT><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
         else if (out_kind == NW_OUT_POWER)
-            cols_kernel<N1, N2, NW_OUT_POWER><<<(unsigned)blocks, 1024, lds, s>>>(f0, nf, B, out);
+            cols_kernel<N1, N2, NW_OUT_POWER><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
         else
-            cols_kernel<N1, N2, NW_OUT_ABS><<<(unsigned)blocks, 1024, lds, s>>>(f0, nf, B, out);
+            cols_kernel<N1, N2, NW_OUT_ABS><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
         return hipGetLastError();
     }
     using CL = Cols<T, N1>;
