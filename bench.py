@@ -286,12 +286,14 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name, dtype
                 text + f' [compute dtype overridden: {dtype}, outputs in {dtype} / its complex type]')
     S = epochs * chans                       # signals on this rank
     F = len(freqs)
-    F_all, by_scales = F, args.shard == 'scales' and world > 1
+    F_all, by_scales = F, shards_scales(args.shard, S, world)
+    f0, f1 = 0, F
     if by_scales:                            # this rank: a contiguous slice of the scales
         from ninwavelets_amd.dist import shard
         f0, f1 = shard(F, rank, world)
         freqs = freqs[f0:f1]
         F = f1 - f0
+    slices = gather_slices(dist, (f0, f1)) if by_scales else None
     C = min((args.chunk if overrides else None) or DEFAULT_CHUNK.get(cfg_name, 256), S)
     f64 = dtype == 'float64'
     x = synth_device(torch, S, n, seed=1000 + (0 if by_scales else rank), device=dev,
@@ -337,12 +339,36 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name, dtype
     res = {'value': points / el, 'ms_per_step': el / args.steps * 1e3, 'dtype': 'f64' if f64 else 'f32',
            'workload': text, 'kind': kind, 'epochs': epochs * (1 if by_scales else world), 'chans': chans,
            'n': n, 'freqs': freqs, 'F': F, 'F_all': F_all, 'out_kind': out_kind, 'chunk': C,
-           'by_scales': by_scales, 'dtype_name': dtype}
+           'by_scales': by_scales, 'dtype_name': dtype, 'scale_slices': slices,
+           'scaling': 'strong' if by_scales else 'weak', 'parallelism': parallelism_of(by_scales, world)}
     extra = roofline_of(args, cfg_name, st, S, F, n, C, out_kind, dtype, esz, el, L) if rank == 0 else {}
     plan.close()
     del bufs, x
     torch.cuda.empty_cache()
     return res, st, extra
+
+
+def shards_scales(shard: str, nsig: int, world: int) -> bool:
+    """Whether the ranks split the scale list (strong scaling) rather than the signals.
+    'auto': the scales exactly when a rank's share of the config is ONE signal (C5: 1 x 2^24,
+    which cannot shard by signal -- SURVEY §8e splits its 512 scales over the GPUs)."""
+    if world <= 1:
+        return False
+    return shard == 'scales' or (shard == 'auto' and nsig == 1)
+
+
+def parallelism_of(by_scales: bool, world: int) -> str:
+    return (f'scales{world} (each rank a contiguous slice of the scales of the same signal, '
+            f'no collective)' if by_scales else f'dp{world} (signals sharded, no collective)')
+
+
+def gather_slices(dist, sl):
+    """Every rank's [f0, f1) scale slice, in rank order (rank 0 reports them)."""
+    if not dist.is_initialized():
+        return [list(sl)]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, list(sl))
+    return out
 
 
 def roofline_of(args, cfg_name, st, S, F, n, C, out_kind, dtype, esz, el, L):
@@ -440,7 +466,8 @@ def roofline_of(args, cfg_name, st, S, F, n, C, out_kind, dtype, esz, el, L):
 
 
 # extra legs of the default line: key -> (config, compute dtype)
-LEGS = {'fp64': ('c4', 'float64'), 'c3': ('c3', 'float32'), 'c5': ('c5', 'float32'), 'c5_fp64': ('c5', 'float64')}
+LEGS = {'fp64': ('c4', 'float64'), 'c2': ('c2', 'float32'), 'c3': ('c3', 'float32'), 'c5': ('c5', 'float32'),
+        'c5_fp64': ('c5', 'float64')}
 
 
 def leg_fields(r, st, ex):
@@ -449,7 +476,9 @@ def leg_fields(r, st, ex):
     the end-to-end figure against the path's minimum traffic."""
     d = {'value': r['value'], 'unit': 'points/s', 'ms_per_step': r['ms_per_step'], 'dtype': r['dtype'],
          'workload': r['workload'], 'output': r['out_kind'], 'chunk_signals': r['chunk'], 'engine': st['engine'],
-         'roofline': ex['roofline']}
+         'scaling': r['scaling'], 'parallelism': r['parallelism'], 'roofline': ex['roofline']}
+    if r['scale_slices'] is not None:
+        d['scale_slices'] = r['scale_slices']
     for k in ('roofline_rows', 'valu_roofline', 'end_to_end_min_traffic', 'computed_rows', 'stage_ms_per_step'):
         if k in ex:
             d[k] = ex[k]
@@ -475,10 +504,11 @@ def main(argv=None):
     ap.add_argument('--wavelet', default=None, choices=['morse', 'morlet', 'shannon'],
                     help="override the config's wavelet (C5 is 'Shannon + Morse': --config c5 "
                          "--wavelet shannon is its Shannon line)")
-    ap.add_argument('--shard', default='signals', choices=['signals', 'scales'],
+    ap.add_argument('--shard', default='auto', choices=['auto', 'signals', 'scales'],
                     help='what the ranks split: signals (weak scaling, every rank its own epochs) '
                          'or the scale list of the same signals (strong scaling; the C5 split for '
-                         'one long signal, SURVEY §8e)')
+                         'one long signal, SURVEY §8e); auto = scales for the one-signal config (C5), '
+                         'signals otherwise')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-fp64', action='store_true',
                     help='skip the fp64 leg (the same workload at the reference\'s complex128 precision, '
@@ -542,8 +572,10 @@ def main(argv=None):
     # The default (C4) line also carries BASELINE.json's other headline workloads, each measured
     # in this same run after the previous leg's buffers are freed, with its own roofline:
     #   fp64: C4 at the reference's precision (complex128 out, base.py:399-406);
+    #   c2:   Morlet cwt 64 x 16384 x 128 (wavelets.py:132-136);
     #   c3:   Morse power 512 x 64 x 4096 x 256 (the fused |.|^2 path, base.py:409-425);
-    #   c5:   Morse cwt 1 x 2^24 x 512, fp32 and fp64 (the long-signal regime, base.py:404-406).
+    #   c5:   Morse cwt 1 x 2^24 x 512, fp32 and fp64 (the long-signal regime, base.py:404-406);
+    #         at N > 1 ranks its 512 scales are split over the ranks (strong scaling).
     default_line = (args.config == 'c4' and res['dtype'] == 'f32' and not args.dtype and not args.output and
                     not args.samples and not args.wavelet and not args.chunk)
     want = [l for l in args.legs.split(',') if l and l != 'none']
@@ -575,14 +607,13 @@ def main(argv=None):
             'metric': 'CWT throughput (epochs*chans*samples*freqs)/s',
             'value': res['value'], 'unit': 'points/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': res['ms_per_step'], 'higher_is_better': True,
-            'scaling': 'strong' if res['by_scales'] else 'weak', 'vs_baseline': None, 'dtype': res['dtype'],
+            'scaling': res['scaling'], 'vs_baseline': None, 'dtype': res['dtype'],
             'data': 'synthetic',
             'config': {'workload': res['workload'], 'wavelet': res['kind'], 'epochs': res['epochs'],
                        'chans': res['chans'], 'samples': res['n'], 'freqs': res['F_all'], 'output': res['out_kind'],
                        'engine': st['engine'], 'chunk_signals': res['chunk'],
-                       'parallelism': (f'scales{world} (each rank a contiguous slice of the scales, '
-                                       f'no collective)' if res['by_scales'] else
-                                       f'dp{world} (signals sharded, no collective)'),
+                       'parallelism': res['parallelism'],
+                       **({'scale_slices': res['scale_slices']} if res['scale_slices'] else {}),
                        **({'backend': backend, 'same_device': True} if args.same_device else {}),
                        **({'process_group': dist.get_backend()} if dist.is_initialized() else {})},
             'roofline': roof, **extra, 'fp64': fp64, **leg_out, 'cpu_baseline': cpu, 'cpu_baseline_pool': cpu_pool,
@@ -605,11 +636,17 @@ def max_over_ranks(torch, dist, el, device):
 
 def dry_run(args, torch, dist, world, rank, backend, timeout=None):
     """The multi-rank flow without a GPU: process group, warmup, barrier-bracketed timed
-    steps (a fixed CPU stand-in per step), MAX over ranks, rank 0's line.  Its value is
-    not a measurement; it proves the launcher and the rank plumbing (tests)."""
+    steps (a fixed CPU stand-in per step), MAX over ranks, rank 0's line, and the same
+    signal / scale partition run_leg takes (C5's scale slices gathered from every rank).
+    Its value is not a measurement; it proves the launcher and the rank plumbing (tests)."""
     if world > 1:
         dist.init_process_group(backend, **({'timeout': timeout} if timeout else {}))
     kind, epochs, chans, n, freqs, out_kind, dtype, text = CONFIGS[args.config]
+    by_scales = shards_scales(args.shard, epochs * chans, world)
+    slices = None
+    if by_scales:
+        from ninwavelets_amd.dist import shard
+        slices = gather_slices(dist, shard(len(freqs), rank, world))
 
     def step():
         time.sleep(0.01 * (1 + rank))        # ranks of unequal speed: the max must win
@@ -631,10 +668,12 @@ def dry_run(args, torch, dist, world, rank, backend, timeout=None):
         print(json.dumps({
             'metric': 'CWT throughput (epochs*chans*samples*freqs)/s', 'value': None, 'unit': 'points/s',
             'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': el / max(1, args.steps) * 1e3, 'higher_is_better': True, 'scaling': 'weak',
+            'ms_per_step': el / max(1, args.steps) * 1e3, 'higher_is_better': True,
+            'scaling': 'strong' if by_scales else 'weak',
             'vs_baseline': None, 'dtype': 'f64' if dtype == 'float64' else 'f32',
             'data': 'dry run: no GPU, no kernels', 'backend': backend,
-            'config': {'workload': text, 'parallelism': f'dp{world}'}}), flush=True)
+            'config': {'workload': text, 'parallelism': f'scales{world}' if by_scales else f'dp{world}',
+                       **({'scale_slices': slices} if slices else {})}}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0

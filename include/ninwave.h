@@ -270,6 +270,13 @@ int nw_make_wavelets(int device, int kind, const double* params, int nparams, co
  * copy-out.  nw_host_free takes exactly a pointer nw_host_alloc returned. */
 int nw_host_alloc(int64_t bytes, void** ptr);
 int nw_host_free(void* ptr);
+/* Advise a pageable host buffer the CALLER has just allocated for a result onto transparent
+ * huge pages (madvise MADV_HUGEPAGE over its whole 2 MiB pages; no reference counterpart:
+ * the drop-in classes call it for the fresh arrays they return when the page-locked pool is
+ * full, ninwavelets_amd/engine.py).  A fresh array is then faulted in 2 MiB at a time during
+ * the copy-out instead of 4 KiB.  nw_execute never changes the page policy of the memory it
+ * is handed.  *advised (may be NULL) receives the bytes advised (0 below one huge page). */
+int nw_host_advise(void* ptr, int64_t bytes, int64_t* advised);
 
 int nw_plan_set_stream(nw_plan* plan, void* hip_stream);   /* NULL: the plan's own stream */
 /* The hipStream_t the plan currently launches on (for event ordering with the caller's

@@ -95,6 +95,7 @@ SIGNATURES = [
                                         ctypes.POINTER(ctypes.c_int64)]),
     ('nw_host_alloc', ctypes.c_int, [_I64, ctypes.POINTER(_P)]),
     ('nw_host_free', ctypes.c_int, [_P]),
+    ('nw_host_advise', ctypes.c_int, [_P, _I64, ctypes.POINTER(_I64)]),
     ('nw_plan_set_stream', ctypes.c_int, [_P, _P]),
     ('nw_plan_get_stream', ctypes.c_int, [_P, ctypes.POINTER(_P)]),
     ('nw_plan_sync', ctypes.c_int, [_P]),
@@ -124,8 +125,17 @@ def lib():
                               '`python -c "import __graft_entry__ as g; g.build()"` '
                               'or `make -C ninwavelets_amd/csrc`')
         handle = ctypes.CDLL(LIB_PATH)
+        # the product library must export every entry point; a diagnostic build of an older
+        # tree (NINWAVE_LIB, tools/ab.sh A/B against a past round) may lack the newer ones,
+        # which then stay unbound (calling one raises AttributeError)
+        product = os.path.abspath(LIB_PATH) in (os.path.join(_HERE, 'libninwave.so'),
+                                                os.path.join(_HERE, 'libninwave_debug.so'))
         for name, res, args in SIGNATURES:
-            fn = getattr(handle, name)
+            fn = getattr(handle, name, None)
+            if fn is None:
+                if product:
+                    raise ImportError(f'{LIB_PATH} does not export {name}: rebuild it')
+                continue
             fn.restype = res
             fn.argtypes = args
         _lib = handle

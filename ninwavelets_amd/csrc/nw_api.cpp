@@ -1121,6 +1121,7 @@ int nw_plan_set_wavelet(nw_plan* p, int kind, const double* params, int nparams,
         d.r = nparams > 1 ? params[1] : 3.0;
         d.b_over_r = d.b / d.r;
         for (int i = 0; i < F; ++i) xstep[i] = (float)(grid->delta / freqs[i]);
+        d.morse_ovf = nw::host::morse_may_overflow(d.b, d.r, grid->delta, grid->len_valid, freqs, F) ? 1 : 0;
     } else if (kind == NW_MORLET) {
         d.sigma = nparams > 0 ? params[0] : 7.0;
         const bool gabor = nparams > 1 && params[1] != 0.0;
@@ -1274,11 +1275,10 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     if (host && p->engine == NW_ENGINE_FUSED) NW_TRY(ensure(&p->d_out, &p->d_out_bytes, (size_t)p->max_batch * row_out));
     if (host && p->engine == NW_ENGINE_ROCFFT && out_kind == NW_OUT_CWT) NW_TRY(need_Y(p));
     // (rocFFT engine, host CWT: the complex result is read back straight from d_Y)
-    // a page-locked destination (nw_host_alloc) is written by DMA directly; a fresh pageable
-    // array (the reference returns a new one per call) faults in on huge pages where the
-    // kernel grants them, not 4 KiB at a time inside the copy-out
+    // a page-locked destination (nw_host_alloc) is written by DMA directly (a fresh pageable
+    // array the caller allocated may have been advised onto huge pages by it, nw_host_advise;
+    // the caller's memory policy is never changed here)
     const bool direct = host && host_pinned(out, (size_t)nsig * row_out);
-    if (host && !direct) nw::host::advise_output((char*)out, (size_t)nsig * row_out);
 
     for (int64_t s0 = 0; s0 < nsig; s0 += p->max_batch) {
         const int64_t c = std::min<int64_t>(p->max_batch, nsig - s0);
@@ -1720,6 +1720,13 @@ int nw_host_alloc(int64_t bytes, void** ptr) {
     NW_HIP(hipHostMalloc(ptr, (size_t)bytes, hipHostMallocDefault));
     std::lock_guard<std::mutex> lk(g_host_mu);
     g_host_bufs[(uintptr_t)*ptr] = (size_t)bytes;
+    return NW_OK;
+}
+
+int nw_host_advise(void* ptr, int64_t bytes, int64_t* advised) {
+    if (!ptr || bytes < 0) return fail(NW_E_INVALID, "nw_host_advise: bad argument");
+    const size_t a = nw::host::advise_output(reinterpret_cast<char*>(ptr), (size_t)bytes);
+    if (advised) *advised = (int64_t)a;
     return NW_OK;
 }
 

@@ -172,6 +172,16 @@ void parallel_copy(char* dst, const char* src, size_t bytes, unsigned max_thread
     for (auto& t : th) t.join();
 }
 
+bool morse_may_overflow(double b, double r, double delta, int64_t len_valid, const double* freqs, int nfreq) {
+    if (r != 0.0 && b / r * 1.4426950408889634 >= 1000.0) return true;      // exp((b/r)(1 - x^r)) near x = 0
+    double fmin = 0.0;
+    for (int i = 0; i < nfreq; ++i)
+        if (freqs[i] > 0.0 && (fmin == 0.0 || freqs[i] < fmin)) fmin = freqs[i];
+    if (fmin == 0.0 || len_valid < 2 || b <= 0.0) return false;
+    const double xmax = (double)(len_valid - 1) * delta / fmin;
+    return xmax > 1.0 && b * std::log2(xmax) >= 1000.0;
+}
+
 size_t advise_output(char* dst, size_t bytes) {
     const size_t huge = size_t(2) << 20;
     const uintptr_t b = (uintptr_t)dst, e = b + bytes;

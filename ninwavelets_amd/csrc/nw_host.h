@@ -63,6 +63,10 @@ void parallel_copy(char* dst, const char* src, size_t bytes, unsigned max_thread
 // 3 ms; populating ahead (MADV_POPULATE_WRITE) was slower than faulting inside the copy.
 // Returns the advised bytes (0: range below one huge page).
 size_t advise_output(char* dst, size_t bytes);
+// Whether some bin x = j * delta / f (j < len_valid) of a Morse plan comes within 2^24 of the
+// fp64 overflow of the reference's x^b (or its exp term: b/r > 709): the rows then take the
+// overflow-checked forms, which reproduce the reference's inf / NaN (wavelets.py:65-74)
+bool morse_may_overflow(double b, double r, double delta, int64_t len_valid, const double* freqs, int nfreq);
 
 }  // namespace host
 }  // namespace nw

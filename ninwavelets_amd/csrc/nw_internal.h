@@ -33,6 +33,9 @@ struct WDesc {
     double  scale;      // 1/n
     // Morse (wavelets.py:65-74)
     double  b, r, b_over_r;
+    // 1 when some Morse bin of the plan overflows the reference's fp64 x^b or exp term (large
+    // b, tiny f): the rows then take the overflow-checked forms (morse_special)
+    int     morse_ovf;
     // Morlet (wavelets.py:118-136): cpi = c * pi^(-1/4), kappa = k
     double  sigma, cpi, kappa;
     // per-frequency device arrays [nfreq]
@@ -69,10 +72,31 @@ __device__ __forceinline__ double psi_f64(const WDesc& d, int fi, int64_t j) {
 // log2(psi/2) = b*log2(x) + (b/r)*log2(e)*(1 - x^r).  Contractions are explicit so the W
 // table (wtable_kernel), the two-pass row evaluator (RowW) and the fused kernel's in-register
 // W tail produce the same bits in every compilation context.
+// The reference evaluates 2 * (x^b * exp((b/r)(1 - x^r))) in fp64 (wavelets.py:65-74): where a
+// factor overflows (x^b for large b and x = nu / f >> 1, or exp for b/r > 709), the product is
+// inf, or NaN (inf * 0) when the other factor underflowed to 0 -- and a NaN bin makes the whole
+// row NaN (ifft).  morse_special gives that value from the two factors' log magnitudes (lp of
+// x^b, lq of the exp term, log base 2^(1/LN)): +inf, NaN, or 0 when neither overflows.
+template <typename F>
+__device__ __forceinline__ bool morse_special(F lp, F lq, F lmax, F lmin_p, F lmin_q, F* v) {
+    const bool p_inf = lp >= lmax, q_inf = lq >= lmax;
+    if (!(p_inf || q_inf)) return false;
+    *v = ((p_inf && lq < lmin_q) || (q_inf && lp < lmin_p)) ? (F)__builtin_nan("") : (F)__builtin_inf();
+    return true;
+}
+// CHECK: apply the reference's overflow semantics (tables, and rows of plans with morse_ovf)
+template <bool CHECK = true>
 __device__ __forceinline__ float morse_f32(float x, float b, float c1, float rr) {
     const float lx = __log2f(x);
-    const float e2 = __builtin_fmaf(b, lx, c1 * (1.0f - exp2f(rr * lx)));   // the contraction clang chose for the plain expression
-    return 2.0f * exp2f(e2);
+    const float lq = c1 * (1.0f - exp2f(rr * lx));
+    const float e2 = __builtin_fmaf(b, lx, lq);   // the contraction clang chose for the plain expression
+    float v = 2.0f * exp2f(e2);
+    if constexpr (CHECK) {
+        // fp64 thresholds in log2: overflow at 2^1024, x^b underflows below 2^-1074, exp below 2^-1075
+        float sp;
+        if (morse_special<float>(b * lx, lq, 1024.0f, -1074.0f, -1075.0f, &sp)) v = sp;
+    }
+    return v;
 }
 __device__ __forceinline__ float morse_c1_f32(const WDesc& d) { return (float)(d.b_over_r * 1.4426950408889634); }
 

@@ -113,6 +113,10 @@ template <typename T, int KIND> struct RowW;
 // instantiation of its own (host dispatch, morse_fast_of), since the general log-domain form's
 // ocml constants beside it spill
 constexpr int kMorseFast = 100;
+// fp32 Morse rows of a plan where some bin overflows the reference's fp64 factors
+// (WDesc::morse_ovf): the overflow-checked form (its own instantiation, so the default rows
+// carry no check)
+constexpr int kMorseOvf = 101;
 template <int KIND> struct RowW<float, KIND> {
     float xs, b, c1, rr, cpi, sigma, kappa, scale;
     int off, lenv, jlim;
@@ -139,10 +143,10 @@ template <int KIND> struct RowW<float, KIND> {
     __device__ __forceinline__ float operator()(int j) const {
         if ((unsigned)j >= (unsigned)lenv) return 0.0f;
         float psi;
-        if constexpr (KIND == NW_MORSE) {
+        if constexpr (KIND == NW_MORSE || KIND == kMorseOvf) {
             const float x = (float)j * xs;
             if (!(x > 0.0f)) return 0.0f;
-            psi = morse_f32(x, b, c1, rr);
+            psi = morse_f32<KIND == kMorseOvf>(x, b, c1, rr);
         } else if constexpr (KIND == NW_MORLET) {
             const float x = (float)j * xs;
             const float a = sigma - x;
@@ -242,7 +246,12 @@ template <int KIND> struct RowW<double, KIND> {
                 psi = 2.0 * (xb * exp_rows(bor * (1.0 - x * x * x)));
             } else {
                 const double lx = log(x);
-                psi = 2.0 * exp(b * lx + bor * (1.0 - exp(r * lx)));
+                const double lq = bor * (1.0 - exp(r * lx));
+                psi = 2.0 * exp(b * lx + lq);
+                // the reference's inf / NaN where a factor overflows (morse_special; ln thresholds)
+                double sp;
+                if (morse_special<double>(b * lx, lq, 709.782712893384, -744.4400719213812, -745.1332191019412, &sp))
+                    psi = sp;
             }
         } else if constexpr (KIND == NW_MORLET) {
             const double nu = (double)(int64_t)j * delta;
@@ -410,6 +419,18 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
 // time: 32-lane groups cover >= 16 consecutive columns (fp32), so reads are conflict-free
 // and writes at most 2-way (free for ds_write_b32, MI355X_MICROARCH.md §LDS); fp64 lanes
 // read 8 B each, so C >= 8 columns keep a 32-lane group on consecutive positions.
+// NW_ABL_COLS_STREAM (diagnostic, wrong results): the column kernels as a pure stream -- the
+// pass-0 B loads and the last pass's y stores at exactly the product's addresses and widths,
+// with no twiddles, FFT arithmetic or LDS exchanges between them: the floor the column pass's
+// access pattern alone reaches (tools/ab.sh next to the product)
+#ifdef NW_ABL_COLS_STREAM
+#ifndef NW_ABL_COLS_NOFFT
+#define NW_ABL_COLS_NOFFT
+#endif
+#ifndef NW_ABL_COLS_NOTW
+#define NW_ABL_COLS_NOTW
+#endif
+#endif
 template <typename T, int N1> struct Cols {
     static constexpr int E = kColE<T>;
     static constexpr int U = N1 / E;                 // threads per column
@@ -635,7 +656,11 @@ __device__ __forceinline__ void colp_passes(C2<f2>* v, f2* lds, int u, int cp, v
     using G = typename CL::G;
     constexpr int U = CL::U;
     constexpr int R = G::radix(P), NS = G::ns(P), Q = CL::E / R;
+#ifdef NW_ABL_COLS_STREAM
+    if constexpr (false) {
+#else
     if constexpr (P > 0) {
+#endif
         constexpr int LR = ilog2<R>();
         lds_barrier();
         colp_write<N1, P - 1, 0>(v, lds, u, cp);
@@ -702,14 +727,21 @@ __global__ __launch_bounds__(ColsP<N1>::THREADS, ColsP<N1>::THREADS / 256) void 
         const int k1 = u + U * r;
         using V4 = float __attribute__((ext_vector_type(4)));
         const V4 b4 = *reinterpret_cast<const V4*>(at(bf, boff, (uint32_t)(U * r * N2 * sizeof(C2<float>))));
+#ifdef NW_ABL_COLS_STREAM
+        (void)k1;
+        v[r] = C2<f2>{f2{b4.x, b4.z}, f2{b4.y, b4.w}};
+#else
         const uint32_t m0 = (uint32_t)col * (uint32_t)k1;                 // n2 k1 < n <= 2^24
         constexpr float inv_n = 1.0f / (float)n;                          // exact: power of two
         const float r0 = (float)m0 * inv_n, r1 = (float)(m0 + (uint32_t)k1) * inv_n;
         const C2<f2> w{f2{__builtin_amdgcn_cosf(r0), __builtin_amdgcn_cosf(r1)},
                        f2{__builtin_amdgcn_sinf(r0), __builtin_amdgcn_sinf(r1)}};
         v[r] = cmul(C2<f2>{f2{b4.x, b4.z}, f2{b4.y, b4.w}}, w);
+#endif
     }
+#ifndef NW_ABL_COLS_STREAM
     idft_br<f2, E>(v);
+#endif
     using O = typename OutT<OUT, float>::type;
     void* orow = reinterpret_cast<char*>(out) + (int64_t)(f0 + fl) * n * (int64_t)sizeof(O);
     const uint32_t ooff = ((uint32_t)col + (uint32_t)u * N2) * (uint32_t)sizeof(O);
@@ -867,7 +899,7 @@ namespace {
 // the fp64 row pass's fast Morse form applies (RowW<double, kMorseFast>)
 bool morse_fast_of(const WDesc& d) {
     const double b2 = 2.0 * d.b;
-    return d.kind == NW_MORSE && d.r == 3.0 && b2 >= 0.0 && b2 < 128.0 && b2 == (double)(int)b2;
+    return d.kind == NW_MORSE && !d.morse_ovf && d.r == 3.0 && b2 >= 0.0 && b2 < 128.0 && b2 == (double)(int)b2;
 }
 
 template <typename T>
@@ -883,6 +915,8 @@ hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, 
                 case NW_MORSE:                                                                               \
                     if constexpr (sizeof(T) == 8)                                                            \
                         if (morse_fast_of(d)) return launch_row_pass<T, NN, EE, kMorseFast>(d, f0, nf, sp.n1, Xt, B, km, s); \
+                    if constexpr (sizeof(T) == 4)                                                            \
+                        if (d.morse_ovf) return launch_row_pass<T, NN, EE, kMorseOvf>(d, f0, nf, sp.n1, Xt, B, km, s); \
                     return launch_row_pass<T, NN, EE, NW_MORSE>(d, f0, nf, sp.n1, Xt, B, km, s);             \
                 case NW_MORLET: return launch_row_pass<T, NN, EE, NW_MORLET>(d, f0, nf, sp.n1, Xt, B, km, s);   \
                 case NW_SHANNON: return launch_row_pass<T, NN, EE, NW_SHANNON>(d, f0, nf, sp.n1, Xt, B, km, s); \

@@ -54,15 +54,25 @@ class HostPool:
     by DMA directly.  A pooled result is an ordinary numpy array owning its buffer: when the
     caller drops it (and every view of it), the buffer returns to the pool for the next
     result of the same size.  At most ``cap`` bytes are page-locked at a time (results the
-    caller keeps count too); past that, results fall back to np.empty.  ``min_bytes``: smaller
-    results are not worth a page-locked buffer."""
+    caller keeps count too); past that, results are fresh pageable arrays advised onto huge
+    pages (nw_host_advise).  ``min_bytes``: smaller results are not worth a page-locked buffer.
 
-    def __init__(self, cap: int, min_bytes: int = 32 << 20, keep_free: int = 2, alloc=None, free=None):
+    Released buffers are handed back by a weakref finalizer, which may run inside a garbage
+    collection triggered anywhere -- including inside this pool's own locked region.  The
+    finalizer therefore never takes the lock or calls into the library: it only appends
+    (ptr, nbytes) to a deque (thread-safe append), and the pool drains that queue at the top
+    of its next take, outside any finalizer."""
+
+    def __init__(self, cap: int, min_bytes: int = 32 << 20, keep_free: int = 2, alloc=None, free=None,
+                 advise=None):
+        import collections
         import threading
         self.cap, self.min_bytes, self.keep_free = int(cap), int(min_bytes), int(keep_free)
         self._alloc, self._free_fn = alloc or self._nw_alloc, free or self._nw_free
+        self._advise = advise if advise is not None else self._nw_advise
         self._lock = threading.Lock()
         self._free: dict = {}            # nbytes -> [ptr]
+        self._returned = collections.deque()   # (ptr, nbytes) released by finalizers, not yet filed
         self.held = 0                    # page-locked bytes, in use or free
 
     @staticmethod
@@ -75,10 +85,36 @@ class HostPool:
     def _nw_free(ptr):
         L.check(L.lib().nw_host_free(ctypes.c_void_p(ptr)))
 
+    @staticmethod
+    def _nw_advise(arr):
+        L.check(L.lib().nw_host_advise(ctypes.c_void_p(arr.ctypes.data), int(arr.nbytes), None))
+
     def free_bytes(self) -> int:
-        return sum(n * len(v) for n, v in self._free.items())
+        self._drain()
+        with self._lock:
+            return sum(n * len(v) for n, v in self._free.items())
+
+    def _drain(self):
+        """File the buffers finalizers returned: keep up to keep_free per size, free the rest
+        (the library calls happen outside the lock)."""
+        drop = []
+        with self._lock:
+            while self._returned:
+                ptr, nbytes = self._returned.popleft()
+                lst = self._free.get(nbytes)
+                if lst is None:
+                    lst = self._free[nbytes] = []
+                if len(lst) < self.keep_free:
+                    lst.append(ptr)
+                else:
+                    self.held -= nbytes
+                    drop.append(ptr)
+        for ptr in drop:
+            self._free_fn(ptr)
 
     def _take(self, nbytes):
+        self._drain()
+        drop = []
         with self._lock:
             lst = self._free.get(nbytes)
             if lst:
@@ -86,11 +122,15 @@ class HostPool:
             # make room: drop free buffers of other sizes first
             for n in list(self._free):
                 while self._free[n] and self.held + nbytes > self.cap:
-                    self._free_fn(self._free[n].pop())
+                    drop.append(self._free[n].pop())
                     self.held -= n
-            if self.held + nbytes > self.cap:
-                return None
-            self.held += nbytes
+            ok = self.held + nbytes <= self.cap
+            if ok:
+                self.held += nbytes
+        for ptr in drop:
+            self._free_fn(ptr)
+        if not ok:
+            return None
         try:
             return self._alloc(nbytes)
         except Exception:
@@ -99,13 +139,8 @@ class HostPool:
             return None
 
     def _release(self, ptr, nbytes):
-        with self._lock:
-            lst = self._free.setdefault(nbytes, [])
-            if len(lst) < self.keep_free:
-                lst.append(ptr)
-                return
-            self.held -= nbytes
-        self._free_fn(ptr)
+        # finalizer context: no lock, no library call (see the class docstring)
+        self._returned.append((ptr, nbytes))
 
     def empty(self, shape, dtype) -> np.ndarray:
         """np.empty(shape, dtype), page-locked when large enough and within the cap."""
@@ -116,7 +151,9 @@ class HostPool:
             return np.empty(shape, dtype=dt)
         ptr = self._take(nbytes)
         if ptr is None:
-            return np.empty(shape, dtype=dt)
+            arr = np.empty(shape, dtype=dt)
+            self._advise(arr)                # our own fresh array: huge pages for the copy-out
+            return arr
         owner = _PooledBuffer(ptr, tuple(int(s) for s in shape), dt)
         f = weakref.finalize(owner, self._release, ptr, nbytes)
         f.atexit = False                 # the process is ending: the OS reclaims it
@@ -131,7 +168,32 @@ class _PooledBuffer:
         self.__array_interface__ = {'data': (ptr, False), 'shape': shape, 'typestr': dtype.str, 'version': 3}
 
 
-HOST_POOL = HostPool(int(os.environ.get('NINWAVE_HOST_POOL_BYTES', str(8 << 30))))
+def host_pinned_array(a) -> bool:
+    """Whether numpy array ``a`` (or the array it views) is a pooled page-locked result."""
+    b = a
+    while b is not None:
+        if isinstance(b, _PooledBuffer):
+            return True
+        b = getattr(b, 'base', None)
+    return False
+
+
+def default_pool_cap(total_ram: int | None = None, local_ranks: int | None = None) -> int:
+    """Page-locked bytes one process may pool by default: 8 GiB, at most 1/8 of the host's RAM,
+    shared by the ranks of one node (LOCAL_WORLD_SIZE processes each hold their own pool, so
+    eight ranks of a node pin no more than one process would).  NINWAVE_HOST_POOL_BYTES
+    overrides it."""
+    if total_ram is None:
+        try:
+            total_ram = os.sysconf('SC_PAGE_SIZE') * os.sysconf('SC_PHYS_PAGES')
+        except (ValueError, OSError, AttributeError):
+            total_ram = 64 << 30
+    if local_ranks is None:
+        local_ranks = int(os.environ.get('LOCAL_WORLD_SIZE') or os.environ.get('WORLD_SIZE') or 1)
+    return int(min(8 << 30, total_ram // 8) // max(1, local_ranks))
+
+
+HOST_POOL = HostPool(int(os.environ.get('NINWAVE_HOST_POOL_BYTES') or default_pool_cap()))
 
 
 def _is_device_tensor(a) -> bool:

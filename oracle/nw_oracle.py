@@ -316,7 +316,8 @@ def plugin_row(mode: str, trans_formula, formula, peak_freq, freq: float, sfreq:
         nu = trans_grid(sfreq, real_length, interpolate)
         w = trans_formula(nu, freq)
         return np.hstack((w, np.zeros(len(nu)))) if interpolate else w
-    if mode in ('Reverse', 'Twice'):
+    # (Reverse returned above: base.py:238-250 reaches make_wavelet only for the other modes)
+    if mode == 'Twice':
         t = np.arange(0, sfreq / freq * real_wave_length, 1 / freq)          # base.py:191-194
         w = ifft(trans_formula(t))
         half = int(w.shape[0])

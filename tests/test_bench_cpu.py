@@ -86,3 +86,24 @@ def test_fft_flops_model():
     # 5 n log2 n + 2 n per row; the chirp-z form: two M-point transforms, M = 2^ceil(log2(2n - 1))
     assert bench.fft_flops_per_row(4096, 'nw_fused_pair_kernel') == 5 * 4096 * 12 + 2 * 4096
     assert bench.fft_flops_per_row(1201, 'nw_chirp_kernel') == 2 * 5 * 4096 * 12 + 2 * 1201
+
+
+@pytest.mark.parametrize('gpus', [2, 3])
+def test_c5_ranks_split_the_scales_dry(gpus):
+    """C5 is one 2^24-sample signal per config: at N > 1 ranks the default partition (--shard
+    auto) gives every rank a contiguous slice of the 512 scales of the same signal (strong
+    scaling); the slices, gathered from the ranks themselves, tile [0, 512)."""
+    r = run('--gpus', str(gpus), '--dry-run', '--config', 'c5', '--steps', '1', '--warmup', '0')
+    assert r.returncode == 0, r.stderr
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith('{')][0])
+    assert d['scaling'] == 'strong' and d['config']['parallelism'] == f'scales{gpus}'
+    sl = d['config']['scale_slices']
+    assert len(sl) == gpus and sl[0][0] == 0 and sl[-1][1] == 512
+    assert all(a[1] == b[0] for a, b in zip(sl, sl[1:])) and all(b - a >= 512 // gpus for a, b in sl)
+
+
+def test_partition_rule():
+    assert bench.shards_scales('auto', 1, 8) and not bench.shards_scales('auto', 1, 1)
+    assert not bench.shards_scales('auto', 32768, 8) and bench.shards_scales('scales', 32768, 2)
+    assert not bench.shards_scales('signals', 1, 8)
+    assert set(bench.LEGS) == {'fp64', 'c2', 'c3', 'c5', 'c5_fp64'}

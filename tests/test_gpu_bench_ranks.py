@@ -60,8 +60,12 @@ def test_default_line_carries_c3_and_c5_legs():
     """BASELINE.json's C3 (fused |.|^2, base.py:409-425) and C5 (2^24 samples x 512 scales,
     fp32 and fp64, base.py:404-406) ride on the default line with their own rooflines."""
     d, _ = run_bench('--config', 'c4', '--epochs', '2', '--steps', '1', '--warmup', '1', '--no-cpu-baseline',
-                     '--legs', 'c3,c5,c5_fp64', timeout=600)
+                     '--legs', 'c2,c3,c5,c5_fp64', timeout=600)
     assert d['fp64'] is None
+    c2 = d['c2']                                 # Morlet cwt 64 x 16384 x 128 (wavelets.py:132-136)
+    assert c2['dtype'] == 'f32' and c2['output'] == 'cwt' and c2['roofline']['kernel'] == 'nw_fused_kernel'
+    assert c2['value'] == pytest.approx(64 * 16384 * 128 / (c2['ms_per_step'] * 1e-3), rel=1e-9)
+    assert c2['scaling'] == 'weak' and c2['parallelism'].startswith('dp1')
     c3 = d['c3']
     assert c3['dtype'] == 'f32' and c3['output'] == 'power' and c3['value'] > 0
     assert c3['roofline']['kernel'] == 'nw_fused_pair_kernel' and c3['roofline']['frac'] > 0
@@ -78,6 +82,25 @@ def test_default_line_carries_c3_and_c5_legs():
         assert c5['end_to_end_min_traffic']['bytes_per_step'] == pytest.approx(
             ((1 << 23) + 1) * 2 * esz + 512 * (1 << 24) * 2 * esz)
         assert c5['valu_roofline']['peak'] == peak
+        assert c5['scaling'] == 'weak' and c5['parallelism'].startswith('dp1')     # one rank
+
+
+def test_two_ranks_split_c5_scales_with_kernels():
+    """The driver's N > 1 line on C5 (one 2^24-sample signal, base.py:404-406): each rank
+    computes a contiguous slice of the 512 scales of the SAME signal (strong scaling, SURVEY
+    §8e), with real two-pass launches on both ranks; value = the whole job's points / the
+    slowest rank's time.  C2 rides the same line signal-sharded (weak)."""
+    d, err = run_bench('--gpus', '2', '--backend', 'gloo', '--same-device', '--config', 'c4', '--epochs', '1',
+                       '--steps', '1', '--warmup', '1', '--no-cpu-baseline', '--legs', 'c2,c5', timeout=600)
+    assert d['n_gpus'] == 2 and d['scaling'] == 'weak'
+    c5 = d['c5']['fp32']
+    assert c5['scaling'] == 'strong' and c5['parallelism'].startswith('scales2')
+    assert c5['scale_slices'] == [[0, 256], [256, 512]]
+    assert c5['value'] == pytest.approx((1 << 24) * 512 / (c5['ms_per_step'] * 1e-3), rel=1e-9)
+    assert c5['roofline']['kernel'] == 'cols_kernel'
+    assert d['c2']['scaling'] == 'weak' and d['c2']['parallelism'].startswith('dp2')
+    assert d['c2']['value'] == pytest.approx(2 * 64 * 16384 * 128 / (d['c2']['ms_per_step'] * 1e-3), rel=1e-9)
+    assert err.count('c5: S=1 n=16777216 F=256') == 2, err[-3000:]
 
 
 def test_rccl_single_rank_bench_path():

@@ -200,3 +200,46 @@ def test_large_scale_chunks_are_exact(dtype, monkeypatch):
     st = next(iter(w._plans.values())).stats()
     assert st['launches_rows'] == 2 * 3                   # per signal, ceil(5 / 2) row-pass launches
     np.testing.assert_array_equal(chunked, whole)
+
+
+@pytest.mark.parametrize('b', [0.5, 3.0, 20.0, 63.5, 64.0, 100.0])
+@pytest.mark.parametrize('n', [1 << 15, 1 << 16])
+def test_large_fp64_morse_b_forms(b, n):
+    """The fp64 row pass's Morse forms across their dispatch boundary (nw_large.hip
+    morse_fast_of): r = 3 with 2b a whole number below 128 takes the x^b multiply chain
+    (b = 0.5: the sqrt alone, b = 3 / 20: whole powers, b = 63.5: the longest chain), b = 64
+    and above the log-domain form.  b = 100 with f = 0.5 / 0.8 Hz puts x^b past the fp64 range
+    (x = nu / f up to 2000): the reference's 2 * (x^b * exp(...)) is inf * 0 = NaN there, so
+    those whole rows are NaN (ifft) and the checked form must give the same NaN rows
+    (wavelets.py:65-74).  fp64 1e-12 of each finite row's max."""
+    x = synth(1, n, seed=int(b * 10) + n % 97)[0].astype(np.float64)
+    freqs = np.array([0.5, 0.8, 3.0, 17.0, 60.0, 250.0])
+    w = nw.Morse(1000, b=b, r=3.0)
+    got = w.cwt(x, freqs)
+    assert large_ran(w)
+    with np.errstate(all='ignore'):
+        ref = O.cwt('morse', x, freqs, b=b, r=3.0)
+    nan_rows = np.isnan(ref).any(axis=1)
+    assert nan_rows.any() == (b == 100.0)
+    for f in range(freqs.size):
+        if nan_rows[f]:
+            assert np.isnan(got[f]).all(), (b, freqs[f])
+        else:
+            assert np.isfinite(got[f]).all() and rel_err(got[f], ref[f]) <= 1e-12, (b, freqs[f])
+
+
+@pytest.mark.parametrize('n', [4096, 1 << 15])
+def test_morse_overflow_rows_fp32(n):
+    """fp32 compute (one-pass table at n = 4096, the two-pass rows' checked instantiation at
+    2^15) keeps the reference's NaN rows where x^b overflows fp64 (b = 100, f <= 0.8 Hz) and
+    matches the finite rows at the fp32 tolerance."""
+    x = synth(1, n, seed=n % 89)[0]
+    freqs = np.array([0.5, 0.8, 3.0, 60.0])
+    got = nw.Morse(1000, b=100.0, r=3.0, dtype='float32').cwt(x, freqs)
+    with np.errstate(all='ignore'):
+        ref = O.cwt('morse', x.astype(np.float64), freqs, b=100.0, r=3.0)
+    for f in range(freqs.size):
+        if np.isnan(ref[f]).any():
+            assert np.isnan(got[f]).all(), freqs[f]
+        else:
+            assert rel_err(got[f], ref[f]) <= tol(n), freqs[f]

@@ -254,7 +254,9 @@ def test_host_pool_recycles_and_caps():
         store[b.ctypes.data] = b
         return b.ctypes.data
 
-    pool = HostPool(cap=3 * 4096, min_bytes=1024, keep_free=1, alloc=alloc, free=freed.append)
+    advised = []
+    pool = HostPool(cap=3 * 4096, min_bytes=1024, keep_free=1, alloc=alloc, free=freed.append,
+                    advise=advised.append)
     a = pool.empty((64, 8), np.float64)                  # 4096 B: pooled
     assert a.ctypes.data in store and pool.held == 4096
     a[:] = 1.0
@@ -272,8 +274,60 @@ def test_host_pool_recycles_and_caps():
     assert d.ctypes.data == pa and pool.held == 3 * 4096
     e = pool.empty((64, 8), np.float64)                  # over the cap: an ordinary array
     assert e.ctypes.data not in store and e.shape == (64, 8)
+    assert len(advised) == 1 and advised[0] is e          # our own fresh array: huge-page advice
     s = pool.empty((10,), np.float64)                    # below min_bytes
-    assert s.ctypes.data not in store
+    assert s.ctypes.data not in store and len(advised) == 1
     del b, c, d
     gc.collect()
-    assert len(freed) == 2 and pool.free_bytes() == 4096  # keep_free = 1 per size
+    assert pool.free_bytes() == 4096 and len(freed) == 2  # keep_free = 1 per size
+
+
+def test_host_pool_release_never_takes_the_lock():
+    """A pooled array held by a reference cycle may be collected by a GC that runs anywhere --
+    inside the pool's own locked region included (an allocation there can trigger it).  Its
+    finalizer must not wait for the lock (the old release path deadlocked there); the buffer
+    is filed at the next take."""
+    import gc
+    import threading
+    from ninwavelets_amd.engine import HostPool
+    store = {}
+
+    def alloc(nb):
+        b = np.zeros(nb, dtype=np.uint8)
+        store[b.ctypes.data] = b
+        return b.ctypes.data
+
+    pool = HostPool(cap=4 * 4096, min_bytes=1024, keep_free=2, alloc=alloc, free=lambda p: None,
+                    advise=lambda a: None)
+
+    class Cycle:
+        pass
+
+    c = Cycle()
+    c.me, c.arr = c, pool.empty((512,), np.float64)
+    ptr = c.arr.ctypes.data
+    del c
+    done = threading.Event()
+
+    def collect_under_lock():
+        with pool._lock:
+            gc.collect()              # runs the finalizer of the cycle's pooled array
+        done.set()
+
+    gc.disable()
+    try:
+        th = threading.Thread(target=collect_under_lock, daemon=True)
+        th.start()
+        th.join(timeout=20)
+    finally:
+        gc.enable()
+    assert done.is_set(), 'the finalizer blocked on the pool lock'
+    again = pool.empty((512,), np.float64)                # filed at this take: the same buffer
+    assert again.ctypes.data == ptr and pool.held == 4096
+
+
+def test_default_pool_cap_shares_the_node():
+    from ninwavelets_amd.engine import default_pool_cap
+    assert default_pool_cap(1 << 40, 1) == 8 << 30                 # 8 GiB per process
+    assert default_pool_cap(1 << 40, 8) == 1 << 30                 # eight ranks of a node: 8 GiB in all
+    assert default_pool_cap(16 << 30, 1) == 2 << 30                # at most 1/8 of the host's RAM
