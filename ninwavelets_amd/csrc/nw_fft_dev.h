@@ -457,7 +457,17 @@ template <typename T, int N, int E> struct Tab1 {
     // table (155 KiB) fit the CU's LDS
     // (fp64 at n = 16384, 15.5 KiB beside the 136 KiB image, measured +2.5 % alone and
     // slower than the X LDS-DMA it would share the space with: not kept)
-    static constexpr bool ON = COUNT > 0 && COUNT * (int)sizeof(C2<S>) <= 8192;
+    // fp64 at n = 16384 (one block per CU either way): the 15.5 KiB table beside the 136 KiB
+    // image (155 KiB of the CU's 160), in the translation units that define NW_TAB1_F64_16384
+    // (nw_fused.hip: C4 shape fp64 8.19-8.21 -> 7.96 ms per launch, 0.525 -> 0.541 of HBM peak;
+    // the C5 fp64 row pass +-0 with it and its step 3 % slower, so nw_large.hip keeps the bases;
+    // profiles/r05_f64_tab1_ab.txt)
+#ifdef NW_TAB1_F64_16384
+    static constexpr bool BIG = sizeof(S) == 8 && N == 16384 && E == 32;
+#else
+    static constexpr bool BIG = false;
+#endif
+    static constexpr bool ON = COUNT > 0 && (COUNT * (int)sizeof(C2<S>) <= 8192 || BIG);
     static constexpr int BYTES = ON ? COUNT * (int)sizeof(C2<S>) : 0;
     static_assert((kImgElems<T, N, E> * sizeof(T)) % 16 == 0, "table alignment");
     __device__ static __forceinline__ const C2<S>* table(const T* lds) {

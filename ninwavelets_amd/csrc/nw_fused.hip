@@ -20,6 +20,8 @@
 #include <mutex>
 #include <tuple>
 
+// the fp64 n = 16384 pass-1 twiddle table (Tab1, nw_fft_dev.h) is on in this file's kernels
+#define NW_TAB1_F64_16384 1
 #include "nw_fft_dev.h"
 
 namespace nw {

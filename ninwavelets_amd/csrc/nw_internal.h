@@ -85,12 +85,15 @@ __device__ __forceinline__ bool morse_special(F lp, F lq, F lmax, F lmin_p, F lm
     return true;
 }
 // CHECK: apply the reference's overflow semantics (tables, and rows of plans with morse_ovf)
+// The exponentials are the raw v_exp_f32 (round 5; exp2f wrapped each in a denormal-range
+// compare / select / ldexp): a psi below 2^-126 (1e-38 of the row's peak 2) is 0, which every
+// table, support scan and row evaluator share, so the zeros the pruning relies on agree.
 template <bool CHECK = true>
 __device__ __forceinline__ float morse_f32(float x, float b, float c1, float rr) {
     const float lx = __log2f(x);
-    const float lq = c1 * (1.0f - exp2f(rr * lx));
+    const float lq = c1 * (1.0f - __builtin_amdgcn_exp2f(rr * lx));
     const float e2 = __builtin_fmaf(b, lx, lq);   // the contraction clang chose for the plain expression
-    float v = 2.0f * exp2f(e2);
+    float v = 2.0f * __builtin_amdgcn_exp2f(e2);
     if constexpr (CHECK) {
         // fp64 thresholds in log2: overflow at 2^1024, x^b underflows below 2^-1074, exp below 2^-1075
         float sp;

@@ -113,6 +113,9 @@ template <typename T, int KIND> struct RowW;
 // instantiation of its own (host dispatch, morse_fast_of), since the general log-domain form's
 // ocml constants beside it spill
 constexpr int kMorseFast = 100;
+// ... and its instantiation for the default b = 17.5 (2b = 35): x^17 by four squarings and one
+// multiply at compile time
+constexpr int kMorseFast35 = 102;
 // fp32 Morse rows of a plan where some bin overflows the reference's fp64 factors
 // (WDesc::morse_ovf): the overflow-checked form (its own instantiation, so the default rows
 // carry no check)
@@ -141,9 +144,17 @@ template <int KIND> struct RowW<float, KIND> {
         }
     }
     __device__ __forceinline__ float operator()(int j) const {
+        if constexpr (KIND == NW_MORSE) {
+            // branch-free (round 5): every bin evaluated, the invalid ones (past the row, x <= 0:
+            // a log2 of 0 or below gives 0 or NaN here) selected to 0, so a pass-0 group's
+            // evaluations interleave; the same operations as psi_f32, so the same bits
+            const float x = (float)j * xs;
+            const float psi = morse_f32<false>(x, b, c1, rr) * scale;
+            return ((unsigned)j < (unsigned)lenv && x > 0.0f) ? psi : 0.0f;
+        }
         if ((unsigned)j >= (unsigned)lenv) return 0.0f;
         float psi;
-        if constexpr (KIND == NW_MORSE || KIND == kMorseOvf) {
+        if constexpr (KIND == kMorseOvf) {
             const float x = (float)j * xs;
             if (!(x > 0.0f)) return 0.0f;
             psi = morse_f32<KIND == kMorseOvf>(x, b, c1, rr);
@@ -170,28 +181,42 @@ template <int KIND> struct RowW<float, KIND> {
 // |r| <= ln2 / 2, 2^k * (Taylor polynomial of degree 13: truncation < 5e-18).  Written out
 // here so its constants are plain operands the compiler can keep in SGPRs (ocml's exp keeps
 // ~22 VGPRs of constants hoisted out of the row loop, which spilled every cheaper Morse form)
-// a constant materialised in an SGPR pair at its use (the empty volatile asm is neither
-// hoisted out of the row loop nor moved to VGPRs: one s_mov pair on the scalar unit per use)
-__device__ __forceinline__ double sconst(double c) {
+// The constants are pinned ONCE per row pass in SGPR pairs (ExpK, an empty volatile asm on each
+// at init: opaque, so the compiler neither folds them back into per-use materialisations nor
+// hoists copies into VGPRs) and read as plain SGPR operands of the FMAs.  (Round 4 pinned each
+// constant at its use: an s_mov_b64 copy + an s_nop hazard wait before every FMA of the
+// polynomial -- 974 s_nop in the fp64 row kernel.)
+__device__ __forceinline__ double spin(double c) {
     asm volatile("" : "+s"(c));
     return c;
 }
-__device__ __forceinline__ double exp_rows(double y) {
-    const double yc = fmin(fmax(y, -1100.0), 1100.0);      // k fits an int; NaN -> bound, fixed below
-    const double k = __builtin_rint(yc * sconst(1.4426950408889634074));
-    double rr = fma(-k, sconst(6.93147180369123816490e-01), yc);
-    rr = fma(-k, sconst(1.90821492927058770002e-10), rr);
-    double p = sconst(1.0 / 6227020800.0);                   // 1/13!
-    p = fma(p, rr, sconst(1.0 / 479001600.0));
-    p = fma(p, rr, sconst(1.0 / 39916800.0));
-    p = fma(p, rr, sconst(1.0 / 3628800.0));
-    p = fma(p, rr, sconst(1.0 / 362880.0));
-    p = fma(p, rr, sconst(1.0 / 40320.0));
-    p = fma(p, rr, sconst(1.0 / 5040.0));
-    p = fma(p, rr, sconst(1.0 / 720.0));
-    p = fma(p, rr, sconst(1.0 / 120.0));
-    p = fma(p, rr, sconst(1.0 / 24.0));
-    p = fma(p, rr, sconst(1.0 / 6.0));
+struct ExpK {
+    double log2e, ln2hi, ln2lo, lo;
+    double c[11];                                            // 1/13!, 1/12!, ..., 1/3!
+    __device__ __forceinline__ void init() {
+        log2e = spin(1.4426950408889634074);
+        ln2hi = spin(6.93147180369123816490e-01);
+        ln2lo = spin(1.90821492927058770002e-10);
+        lo = spin(-1100.0);
+        double f = 6227020800.0;                             // 13!
+#pragma unroll
+        for (int i = 0; i < 11; ++i) {
+            c[i] = spin(1.0 / f);
+            f /= (double)(13 - i);
+        }
+    }
+};
+__device__ __forceinline__ double exp_rows(double y, const ExpK& K) {
+    // k fits an int: y is bounded below here (NaN -> the bound, fixed at the end); above by the
+    // fast Morse form's domain, y = (b/r)(1 - x^3) <= b/3 < 21.4 (a select, not fmax: fmax
+    // canonicalises its opaque SGPR operand with two extra v_max per call)
+    const double yc = y > K.lo ? y : K.lo;
+    const double k = __builtin_rint(yc * K.log2e);
+    double rr = fma(-k, K.ln2hi, yc);
+    rr = fma(-k, K.ln2lo, rr);
+    double p = K.c[0];                                       // 1/13!
+#pragma unroll
+    for (int i = 1; i < 11; ++i) p = fma(p, rr, K.c[i]);     // (degree 11: +-0 on the C5 fp64 row pass, round 5)
     p = fma(p, rr, 0.5);
     p = fma(p, rr, 1.0);
     p = fma(p, rr, 1.0);
@@ -200,14 +225,20 @@ __device__ __forceinline__ double exp_rows(double y) {
 }
 
 template <int KIND> struct RowW<double, KIND> {
-    static constexpr bool MORSE = KIND == NW_MORSE || KIND == kMorseFast;
+    static constexpr bool MORSE = KIND == NW_MORSE || KIND == kMorseFast || KIND == kMorseFast35;
     // kMorseFast: x^b by a multiply chain (+ one sqrt for the half) and x^3 by two multiplies,
     // then ONE exp -- 2 x^b exp((b/r)(1 - x^3)), the reference's own factorisation
-    // (wavelets.py:65-74) -- instead of one log and two exps
-    static constexpr bool FAST = KIND == kMorseFast;
-    double delta, f, xs, peak, b, r, bor, sigma, cpi, kappa, scale;
+    // (wavelets.py:65-74) -- instead of one log and two exps.  kMorseFast35 (b = 17.5, round 5)
+    // is branch-free: every bin is evaluated and the invalid ones (j past the row, x <= 0)
+    // selected to 0 at the end, so the evaluations of a pass-0 group interleave (the branches
+    // around each one were s_and_saveexec / s_cbranch pairs that serialised them), with the
+    // sqrt without the compiler's denormal scaling and class checks (x >= delta / f is normal
+    // for every valid bin)
+    static constexpr bool FAST = KIND == kMorseFast || KIND == kMorseFast35;
+    double delta, f, xs, peak, b, r, bor, sigma, cpi, kappa, scale, scale2;
     int off, lenv;
     int bint, bhalf;
+    ExpK ek;
     __device__ static __forceinline__ double pin(double v) {
         const long long u = __double_as_longlong(v);
         const int lo = __builtin_amdgcn_readfirstlane((int)(u & 0xffffffffLL));
@@ -226,12 +257,37 @@ template <int KIND> struct RowW<double, KIND> {
         cpi = d.cpi;
         kappa = d.kappa;
         scale = d.scale;
+        scale2 = 2.0 * d.scale;
         off = (int)d.off;
         lenv = d.len_valid < 0x7fffffff ? (int)d.len_valid : 0x7fffffff;
         bint = FAST ? (int)(2.0 * d.b) / 2 : 0;
         bhalf = FAST ? (int)(2.0 * d.b) & 1 : 0;
+        if constexpr (FAST) ek.init();
+    }
+    // sqrt(x) for normal x > 0 to within an ulp: the rsq estimate and two Newton-Raphson steps
+    // (the compiler's sequence without its denormal scaling and special-value class checks)
+    __device__ static __forceinline__ double sqrt_normal(double x) {
+        const double r = __builtin_amdgcn_rsq(x);
+        double s = x * r, h = 0.5 * r;
+        const double e = fma(-h, s, 0.5);
+        s = fma(s, e, s);
+        h = fma(h, e, h);
+        double d = fma(-s, s, x);
+        s = fma(d, h, s);
+        d = fma(-s, s, x);
+        return fma(d, h, s);
     }
     __device__ __forceinline__ double operator()(int j) const {
+        if constexpr (KIND == kMorseFast35) {
+            // branch-free (the general kMorseFast form below keeps its branches: interleaved,
+            // its runtime chain and sqrt select spilled 236 B)
+            const double x = (double)j * xs;
+            const double x2 = x * x, x4 = x2 * x2, x8 = x4 * x4, x16 = x8 * x8;
+            const double xb = (x16 * x) * sqrt_normal(x);
+            // 2 * (x^b e) * scale: 2 * scale is a power of two, so one multiply by it rounds alike
+            const double psi = (xb * exp_rows(bor * (1.0 - x * x * x), ek)) * scale2;
+            return ((unsigned)j < (unsigned)lenv && x > 0.0) ? psi : 0.0;
+        }
         if ((unsigned)j >= (unsigned)lenv) return 0.0;
         double psi;
         if constexpr (MORSE) {
@@ -243,7 +299,7 @@ template <int KIND> struct RowW<double, KIND> {
                     if (e & 1) xb *= pw;
                     pw *= pw;
                 }
-                psi = 2.0 * (xb * exp_rows(bor * (1.0 - x * x * x)));
+                psi = 2.0 * (xb * exp_rows(bor * (1.0 - x * x * x), ek));
             } else {
                 const double lx = log(x);
                 const double lq = bor * (1.0 - exp(r * lx));
@@ -272,8 +328,16 @@ template <int KIND> struct RowW<double, KIND> {
 // fp64 rows with the same DMA measured no faster (0.94 -> 0.98 ms per launch)
 // (fp64 rows with the DMA, re-measured in round 4 beside the fast Morse form: no gain either,
 // profiles/r04_c5f64_rows_ab.txt)
+// NW_ABL_ROWS_STREAM (diagnostic, wrong results): the row pass as a pure stream -- the pass-0
+// Xt loads (global, no LDS-DMA) and the last pass's B stores at the product's addresses and
+// widths, without W, FFT arithmetic or exchanges: the floor of its write stream
+#ifdef NW_ABL_ROWS_STREAM
+constexpr bool kRowsStream = true;
+#else
+constexpr bool kRowsStream = false;
+#endif
 template <typename T, int E, int KIND>
-constexpr bool kRowsXD = sizeof(T) == 4 && E >= 32 && KIND != NW_TABLE;
+constexpr bool kRowsXD = sizeof(T) == 4 && E >= 32 && KIND != NW_TABLE && !kRowsStream;
 // 4 waves/SIMD; fp64: 2 (twice the registers per element, as nw_fused)
 template <typename T, int N2, int E, int KIND>
 __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
@@ -360,21 +424,24 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
                         const cplx<T> w = wavelet_bin<T>(d, fi, (int64_t)j);
                         v[r] = cmul(C2<T>{w.re, w.im}, xv);
                     } else {
-#ifdef NW_ABL_ROWS_NOW
+#if defined(NW_ABL_ROWS_NOW)
                         const T w = (T)(j & 1);
+#elif defined(NW_ABL_ROWS_STREAM)
+                        (void)j;
+                        const T w = T(1);
 #else
                         const T w = wf(j);
 #endif
                         v[r] = C2<T>{w * xv.re, w * xv.im};
                         // fp64 W: at most 4 evaluations in flight (they hold ~12 VGPRs each)
-                        if constexpr (sizeof(T) == 8 && (KIND == NW_MORSE || KIND == kMorseFast))
+                        if constexpr (sizeof(T) == 8 && (KIND == NW_MORSE || KIND == kMorseFast || KIND == kMorseFast35))
                             if (r % 4 == 3) __builtin_amdgcn_sched_barrier(0);
                     }
                 } else {
                     v[r] = C2<T>{T(0), T(0)};
                 }
             }
-            idft_br<T, E, NZ>(v);
+            if constexpr (!kRowsStream) idft_br<T, E, NZ>(v);
         };
         if (XD && in_lds) {
             if (need <= 4) pass0.template operator()<4, XD>();
@@ -405,7 +472,11 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
         }
         // B rows stored nt (fp64: the 16-B complex128 stores; plain ones made the C5 fp64 step
         // 129.4 ms against 125.3)
-#ifdef NW_B_PLAIN   // diagnostic: B with plain stores (kept in the Infinity Cache when it fits)
+#if defined(NW_ABL_ROWS_STREAM)
+        (void)x;
+        (void)rounds_next;
+        LastStores<T, N2, E, NW_OUT_CWT, kStoreGlobalNt>::all(v, orow, t);
+#elif defined(NW_B_PLAIN)   // diagnostic: B with plain stores (kept in the Infinity Cache when it fits)
         passes_from<T, N2, E, NW_OUT_CWT, 1, XD, kStoreGlobal>(v, lds, t, tw, x, xs_next, orow, nullptr, nullptr, rounds_next);
 #else
         passes_from<T, N2, E, NW_OUT_CWT, 1, XD, kStoreGlobalNt>(v, lds, t, tw, x, xs_next, orow, nullptr, nullptr, rounds_next);
@@ -914,7 +985,9 @@ hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, 
             switch (d.kind) {                                                                                \
                 case NW_MORSE:                                                                               \
                     if constexpr (sizeof(T) == 8)                                                            \
-                        if (morse_fast_of(d)) return launch_row_pass<T, NN, EE, kMorseFast>(d, f0, nf, sp.n1, Xt, B, km, s); \
+                        if (morse_fast_of(d))                                                                \
+                            return d.b == 17.5 ? launch_row_pass<T, NN, EE, kMorseFast35>(d, f0, nf, sp.n1, Xt, B, km, s) \
+                                               : launch_row_pass<T, NN, EE, kMorseFast>(d, f0, nf, sp.n1, Xt, B, km, s);  \
                     if constexpr (sizeof(T) == 4)                                                            \
                         if (d.morse_ovf) return launch_row_pass<T, NN, EE, kMorseOvf>(d, f0, nf, sp.n1, Xt, B, km, s); \
                     return launch_row_pass<T, NN, EE, NW_MORSE>(d, f0, nf, sp.n1, Xt, B, km, s);             \

@@ -7,17 +7,16 @@ launch walks several XCD-tile "G-rounds" (nw_fused.hip: signal groups padded to
 small-batch parity tests (<= 37 signals: G-round 0 only) do not cover it.  Here the bench's
 exact plans run S = chunk + 37 signals (one full chunk, then a ragged tail) and:
 
-- every (signal, scale) row of the complex output is checked against fp64 numpy through
-  its forward FFT: fft(y) must equal W_f * fft(x) (y = ifft(W_f * X), base.py:378-407, with
-  W_f the oracle's cached row, base.py:221-279), as a per-row relative L2 error -- by
-  Parseval that is the row's relative error over all of its points;
+- every point of every (signal, scale) row against y = ifft(W_f * X) (base.py:378-407),
+  W_f the oracle's cached row (base.py:221-279) and X = np.fft.fft(x), the inverse taken in
+  complex128 on the device: the parity contract per signal, and each row on its own scale;
 - every row's energy sum_n |y|^2 (or sum_n of the power output, base.py:409-425) against
   (1/N) sum_k |W_f X|^2 from numpy (Parseval);
 - sampled signals in every G-round and XCD slot of the chunk and in the tail against the
   oracle's full cwt / power (oracle/nw_oracle.py), at the parity tolerances of
   test_gpu_parity.py (fp64 1e-12, fp32 1e-5 of max|ref|, x2 for |.|^2).
 
-The device-side FFT / sums (torch on the GPU) are the checker's arithmetic, in complex128.
+The device-side inverse FFT / sums (torch on the GPU) are the checker's arithmetic, in complex128.
 """
 import os
 import re
@@ -95,22 +94,29 @@ def test_bench_chunk_every_row(n, dtype, chunk, out_kind, kernel):
     Xd = torch.from_numpy(X).to(dev)
     tol = 1e-12 if f64 else 1e-5
 
-    def check_cwt_rows(out):
-        """fft(y) vs W*X for every row, per-row relative L2 (= the row's relative error)."""
-        worst = 0.0
-        for s0 in range(0, S, 32):
-            s1 = min(S, s0 + 32)
-            y = out[s0:s1].to(torch.complex128)
-            ref = Wd[None, :, :] * Xd[s0:s1, None, :]
-            d = torch.linalg.vector_norm(torch.fft.fft(y, dim=-1) - ref, dim=-1)
-            r = torch.linalg.vector_norm(ref, dim=-1)
-            worst = max(worst, float((d / r).max()))
-            e = (y.abs() ** 2).sum(dim=-1).cpu().numpy()
-            np.testing.assert_allclose(e, energy[s0:s1], rtol=4 * tol)
-            del y, ref, d
-        # fp32: a few ulp of rms per point (the kernels' twiddles are v_sin/v_cos, 1.2e-7)
-        assert worst <= (1e-13 if f64 else 2e-6), worst
-        return worst
+    def check_rows(out, power=False):
+        """Every row against y = ifft(W * X) in fp64 on the device: the parity contract per
+        signal (max |dy| <= tol * max|y| over its scales; x2 for |.|^2) and every row on its
+        own scale (max |dy_row| <= 5e-4 * max|y_row| fp32, 1e-10 fp64: a wrong tile, G-round or
+        offset puts an O(1) error into some row), plus each row's Parseval energy."""
+        worst_sig, worst_row = 0.0, 0.0
+        row_tol = 1e-10 if f64 else 5e-4
+        for s0 in range(0, S, 16):
+            s1 = min(S, s0 + 16)
+            ref = torch.fft.ifft(Wd[None, :, :] * Xd[s0:s1, None, :], dim=-1)
+            got = out[s0:s1].to(torch.float64 if power else torch.complex128)
+            if power:
+                ref = ref.abs() ** 2
+            d = (got - ref).abs().amax(dim=-1)                  # (signals, F)
+            m = ref.abs().amax(dim=-1)
+            worst_sig = max(worst_sig, float((d.amax(dim=-1) / m.amax(dim=-1)).max()))
+            worst_row = max(worst_row, float((d / m.clamp_min(1e-300)).max()))
+            e = (got if power else got.abs() ** 2).sum(dim=-1).cpu().numpy()
+            np.testing.assert_allclose(e, energy[s0:s1], rtol=(8 if power else 4) * tol)
+            del ref, got, d, m
+        assert worst_sig <= (2 if power else 1) * tol, worst_sig
+        assert worst_row <= row_tol, worst_row
+        return worst_sig, worst_row
 
     picks = sampled(S, chunk)
     ref_cwt = {s: O.cwt('morse', x[s].astype(np.float64), freqs) for s in picks}
@@ -122,7 +128,7 @@ def test_bench_chunk_every_row(n, dtype, chunk, out_kind, kernel):
         st = plan.stats()
         assert st['engine'] == 'fused' and L.KERNEL_NAMES[st['kernel']] == kernel, st
         assert st['launches_fused'] == 2, st               # the full chunk, then the tail
-        check_cwt_rows(out)
+        check_rows(out)
         for s in picks:
             got = out[s].cpu().numpy()
             ref = ref_cwt[s]
@@ -136,18 +142,17 @@ def test_bench_chunk_every_row(n, dtype, chunk, out_kind, kernel):
         torch.cuda.synchronize()
         st = plan.stats()
         assert st['engine'] == 'fused' and L.KERNEL_NAMES[st['kernel']] == kernel, st
-        e = pw.to(torch.float64).sum(dim=-1).cpu().numpy()
-        np.testing.assert_allclose(e, energy, rtol=8 * tol)
+        check_rows(pw, power=True)
         for s in picks:
             got = pw[s].cpu().numpy()
             ref = np.abs(ref_cwt[s]) ** 2
             assert np.max(np.abs(got - ref)) <= 2 * tol * np.max(ref), s
         # the same plan's complex output over the same chunks (same kernel family and block
-        # map): every row through the FFT check, and power == |cwt|^2 of it
+        # map): every row checked, and power == |cwt|^2 of it
         out = torch.empty((S, F, n), dtype=cdt, device=dev)
         plan.execute(xd, out, out_kind='cwt')
         torch.cuda.synchronize()
-        check_cwt_rows(out)
+        check_rows(out)
         for s0 in range(0, S, 64):
             s1 = min(S, s0 + 64)
             c2 = out[s0:s1].to(torch.complex128).abs() ** 2
