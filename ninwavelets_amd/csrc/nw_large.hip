@@ -40,6 +40,9 @@
 // hits, the row pass loses its Xt reuse across the scales of a tile.
 #include <cstdlib>
 
+#ifdef NW_ROWS_TAB1   // A/B: the fp64 n2 = 16384 pass-1 twiddle table in the row pass too
+#define NW_TAB1_F64_16384 1
+#endif
 #include "nw_fft_dev.h"
 
 namespace nw {
@@ -206,11 +209,16 @@ struct ExpK {
         }
     }
 };
+// FINITE: y is known finite and <= 21.4 (the b = 17.5 rows' valid bins): no NaN pass-through,
+// and the lower bound by one v_max_f64 against a plain constant
+template <bool FINITE = false>
 __device__ __forceinline__ double exp_rows(double y, const ExpK& K) {
     // k fits an int: y is bounded below here (NaN -> the bound, fixed at the end); above by the
     // fast Morse form's domain, y = (b/r)(1 - x^3) <= b/3 < 21.4 (a select, not fmax: fmax
     // canonicalises its opaque SGPR operand with two extra v_max per call)
-    const double yc = y > K.lo ? y : K.lo;
+    double yc;
+    if constexpr (FINITE) yc = fmax(y, -1100.0);
+    else yc = y > K.lo ? y : K.lo;
     const double k = __builtin_rint(yc * K.log2e);
     double rr = fma(-k, K.ln2hi, yc);
     rr = fma(-k, K.ln2lo, rr);
@@ -221,6 +229,7 @@ __device__ __forceinline__ double exp_rows(double y, const ExpK& K) {
     p = fma(p, rr, 1.0);
     p = fma(p, rr, 1.0);
     const double e = ldexp(p, (int)k);
+    if constexpr (FINITE) return e;
     return y == y ? e : y;
 }
 
@@ -237,7 +246,7 @@ template <int KIND> struct RowW<double, KIND> {
     static constexpr bool FAST = KIND == kMorseFast || KIND == kMorseFast35;
     double delta, f, xs, peak, b, r, bor, sigma, cpi, kappa, scale, scale2;
     int off, lenv;
-    int bint, bhalf;
+    int bint, bhalf, jm1;
     ExpK ek;
     __device__ static __forceinline__ double pin(double v) {
         const long long u = __double_as_longlong(v);
@@ -263,6 +272,7 @@ template <int KIND> struct RowW<double, KIND> {
         bint = FAST ? (int)(2.0 * d.b) / 2 : 0;
         bhalf = FAST ? (int)(2.0 * d.b) & 1 : 0;
         if constexpr (FAST) ek.init();
+        jm1 = (xs > 0.0 && lenv > 0) ? lenv - 1 : 0;
     }
     // sqrt(x) for normal x > 0 to within an ulp: the rsq estimate and two Newton-Raphson steps
     // (the compiler's sequence without its denormal scaling and special-value class checks)
@@ -285,8 +295,10 @@ template <int KIND> struct RowW<double, KIND> {
             const double x2 = x * x, x4 = x2 * x2, x8 = x4 * x4, x16 = x8 * x8;
             const double xb = (x16 * x) * sqrt_normal(x);
             // 2 * (x^b e) * scale: 2 * scale is a power of two, so one multiply by it rounds alike
-            const double psi = (xb * exp_rows(bor * (1.0 - x * x * x), ek)) * scale2;
-            return ((unsigned)j < (unsigned)lenv && x > 0.0) ? psi : 0.0;
+            const double psi = (xb * exp_rows<true>(bor * (1.0 - x2 * x), ek)) * scale2;
+            // valid bins 1 <= j < lenv (x > 0 <=> j > 0 with xs > 0; none when xs <= 0: psi = 0
+            // there, heaviside(x, x) of x <= 0): one unsigned compare on integers, j - 1 < jm1
+            return (unsigned)(j - 1) < (unsigned)jm1 ? psi : 0.0;
         }
         if ((unsigned)j >= (unsigned)lenv) return 0.0;
         double psi;
@@ -925,9 +937,9 @@ bool large_supported(int64_t n, int dtype) {
            !(n & (n - 1));
 }
 
-size_t large_scratch_bytes(int64_t n, int nfreq, int dtype) {
+size_t large_scratch_bytes(int64_t n, int nfreq, int dtype, int nb) {
     const size_t per = (size_t)n * cplx_bytes(dtype);
-    return per + (size_t)fchunk_of(n, nfreq, dtype) * per;   // Xt + B
+    return per + (size_t)nb * (size_t)fchunk_of(n, nfreq, dtype) * per;   // Xt + nb x B
 }
 
 size_t large_support_bytes(int nfreq) { return tsplit_offset(nfreq) + kSplitEntries * sizeof(C2<double>); }
@@ -974,10 +986,10 @@ bool morse_fast_of(const WDesc& d) {
 }
 
 template <typename T>
-hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, hipStream_t s) {
+hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, hipStream_t s, int bi) {
     const Split sp = split_of(d.n, sizeof(T) == 4 ? NW_F32 : NW_F64);
     C2<T>* Xt = reinterpret_cast<C2<T>*>(scratch);
-    C2<T>* B = Xt + d.n;
+    C2<T>* B = Xt + d.n + (int64_t)bi * fchunk_of(d.n, d.nfreq, sizeof(T) == 4 ? NW_F32 : NW_F64) * d.n;
 #define NW_ROWS(NN)                                                                                          \
     case NN:                                                                                                 \
         if constexpr (NN <= kMaxN2<T>) {                                                                     \
@@ -1007,9 +1019,10 @@ hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, 
 
 template <typename T>
 hipError_t cols_t(const WDesc& d, int out_kind, int f0, int nf, const void* support, const void* scratch, void* out,
-                  hipStream_t s) {
+                  hipStream_t s, int bi) {
     const Split sp = split_of(d.n, sizeof(T) == 4 ? NW_F32 : NW_F64);
-    const C2<T>* B = reinterpret_cast<const C2<T>*>(scratch) + d.n;
+    const C2<T>* B = reinterpret_cast<const C2<T>*>(scratch) + d.n +
+                     (int64_t)bi * fchunk_of(d.n, d.nfreq, sizeof(T) == 4 ? NW_F32 : NW_F64) * d.n;
     const C2<T>* ts = sizeof(T) == 8 ? reinterpret_cast<const C2<T>*>(reinterpret_cast<const char*>(support) +
                                                                       tsplit_offset(d.nfreq))
                                      : nullptr;
@@ -1029,15 +1042,19 @@ hipError_t cols_t(const WDesc& d, int out_kind, int f0, int nf, const void* supp
 
 // pass 1 for scales [f0, f0 + nf): Xt -> B (both in the scratch)
 hipError_t large_rows(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, hipStream_t s) {
+    return large_rows_b(d, dtype, f0, nf, support, scratch, 0, s);
+}
+hipError_t large_rows_b(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, int bi,
+                        hipStream_t s) {
     const int* km = reinterpret_cast<const int*>(support);
-    return dtype == NW_F32 ? rows_t<float>(d, f0, nf, km, scratch, s) : rows_t<double>(d, f0, nf, km, scratch, s);
+    return dtype == NW_F32 ? rows_t<float>(d, f0, nf, km, scratch, s, bi) : rows_t<double>(d, f0, nf, km, scratch, s, bi);
 }
 
 // pass 2 for scales [f0, f0 + nf): B -> out rows (f, n) of one signal (out: its row 0)
 hipError_t large_cols(const WDesc& d, int dtype, int out_kind, int f0, int nf, const void* support,
-                      const void* scratch, void* out, hipStream_t s) {
-    return dtype == NW_F32 ? cols_t<float>(d, out_kind, f0, nf, support, scratch, out, s)
-                           : cols_t<double>(d, out_kind, f0, nf, support, scratch, out, s);
+                      const void* scratch, void* out, hipStream_t s, int bi) {
+    return dtype == NW_F32 ? cols_t<float>(d, out_kind, f0, nf, support, scratch, out, s, bi)
+                           : cols_t<double>(d, out_kind, f0, nf, support, scratch, out, s, bi);
 }
 
 }  // namespace nw

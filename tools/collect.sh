@@ -5,8 +5,8 @@
 set -eu
 R=${1:-gpurun_out/rec}
 P=profiles
-ROUND=${ROUND:-r04}
-for c in ${CFGS:-c4 c3 c5 c5f64 c4f64}; do
+ROUND=${ROUND:-r05}
+for c in ${CFGS:-c4 c2 c3 c5 c5f64 c4f64}; do
   [ -s $R/bench_$c.json ] || { echo "no bench line for $c"; continue; }
   cp $R/bench_$c.json $P/${ROUND}_bench_$c.json
   st=$(find $R/prof_$c -name '*kernel_stats.csv' | head -1)

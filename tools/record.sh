@@ -1,7 +1,7 @@
 #!/bin/bash
 # Measurement record of the current build: GPU tests, smoke, bench lines, rocprofv3
 # kernel-trace --stats and PMC passes (traffic tied to the engine-source hash) for C4, C3,
-# C5 (fp32, fp64) and the fp64 C4 shape.  Output under $REC (default gpurun_out/rec/); stops at the first
+# C5 (fp32, fp64), C2 and the fp64 C4 shape.  Output under $REC (default gpurun_out/rec/); stops at the first
 # failure; tools/collect.sh copies it into profiles/.  CFGS selects configs, SKIP_TESTS=1 the tests.
 set -u
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
@@ -23,10 +23,11 @@ record() {
     python3 -c "import json; d=json.load(open('$R/pmc_${name}_$k.json')); print('$name $k traffic', d.get('hbm_bytes_per_launch'), 'ms', round(d['profiled_avg_duration_ms'],4), 'clk', round(d.get('effective_clock_ghz',0),3))"
   done
 }
-CFGS=${CFGS:-c4 c3 c5 c5f64 c4f64}
+CFGS=${CFGS:-c4 c2 c3 c5 c5f64 c4f64}
 for c in $CFGS; do
   case $c in
     c4) record c4 "--steps 10 --warmup 3" "--config c4 --steps 2 --warmup 1 --legs none" "nw_fused_kernel" '{"chunk": 512, "n": 16384, "freqs": 256, "out": "cwt", "dtype": "float32"}' || exit $? ;;
+    c2) record c2 "--config c2 --steps 20 --warmup 3" "--config c2 --steps 5 --warmup 1" "nw_fused_kernel" '{"chunk": 64, "n": 16384, "freqs": 128, "out": "cwt", "dtype": "float32"}' || exit $? ;;
     c3) record c3 "--config c3 --steps 5 --warmup 2" "--config c3 --steps 2 --warmup 1" "nw_fused_pair_kernel" '{"chunk": 1024, "n": 4096, "freqs": 256, "out": "power", "dtype": "float32"}' || exit $? ;;
     c5) record c5 "--config c5 --steps 3 --warmup 1" "--config c5 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float32", "scales_per_launch": 64}' || exit $? ;;
     c5f64) record c5f64 "--config c5 --dtype float64 --steps 3 --warmup 1" "--config c5 --dtype float64 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float64", "scales_per_launch": 32}' || exit $? ;;
