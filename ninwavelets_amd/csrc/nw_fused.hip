@@ -69,6 +69,12 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
 // per launch; fp64 has no registers to spare (4 and 8 measured +-0 / slower, with spills);
 // n = 8192 (256-thread blocks) keeps 8: 16 spilled 12-16 B there
 constexpr int kWKeep32 = 16, kWKeep32Small = 8;
+// fp64 n = 16384 (A/B, NW_WKEEP64): the pass-1 twiddle table (Tab1) left 14 VGPRs of the 256
+#ifdef NW_WKEEP64
+constexpr int kWKeep64 = NW_WKEEP64;
+#else
+constexpr int kWKeep64 = 0;
+#endif
 // (W elements beyond kWKeep32 evaluated in registers for Morse rows instead of re-read:
 // C4 3.360-3.368 -> 3.420-3.430 ms per launch; removing those loads altogether (diagnostic)
 // 3.367-3.369: the re-read costs nothing, the evaluation's VALU does)
@@ -164,7 +170,8 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     // E = 32: the first WKEEP elements of W stay in registers for the block (a row pruned to
     // NZ <= WKEEP reads no W per signal; loads issued after the previous signal's stores
     // wait for all of them in the in-order vmcnt queue)
-    constexpr int WKEEP = (!WREG && REALW && sizeof(T) == 4) ? (N >= 16384 ? kWKeep32 : kWKeep32Small) : 0;
+    constexpr int WKEEP = (!WREG && REALW && sizeof(T) == 4) ? (N >= 16384 ? kWKeep32 : kWKeep32Small)
+                        : (!WREG && REALW && sizeof(T) == 8 && N == 16384) ? kWKeep64 : 0;
     WT wk[WKEEP > 0 ? WKEEP : 1];
     if constexpr (WKEEP > 0) {
 #pragma unroll
