@@ -233,9 +233,6 @@ struct nw_plan {
     // host copy of piece i-1 into the caller's pageable array)
     void* pinned[2] = {nullptr, nullptr};
     hipEvent_t pinned_ev[2] = {nullptr, nullptr};
-    // pipelined two-pass form: the column pass on a second stream, two B buffers
-    hipStream_t stream2 = nullptr;
-    hipEvent_t pipe_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};   // rows[2], cols[2], join
 
     // timing
     std::vector<Pending> pending;
@@ -280,7 +277,7 @@ void count_launch(nw_plan* p, int stage) {
 }
 
 template <typename F>
-int staged(nw_plan* p, int stage, F&& fn, hipStream_t on = nullptr) {
+int staged(nw_plan* p, int stage, F&& fn) {
     count_launch(p, stage);
     nw_logf(2, "plan %p: launch %s%s%s", (void*)p, kStageName[stage], stage == ST_FUSED || stage == ST_ROWS ? ": " : "",
             stage == ST_FUSED || stage == ST_ROWS ? kernel_name(p->stats.kernel) : "");
@@ -288,9 +285,9 @@ int staged(nw_plan* p, int stage, F&& fn, hipStream_t on = nullptr) {
     Pending pe{stage, nullptr, nullptr};
     NW_TRY(take_event(p, &pe.a));
     NW_TRY(take_event(p, &pe.b));
-    NW_HIP(hipEventRecord(pe.a, on ? on : p->stream));
+    NW_HIP(hipEventRecord(pe.a, p->stream));
     int r = fn();
-    NW_HIP(hipEventRecord(pe.b, on ? on : p->stream));
+    NW_HIP(hipEventRecord(pe.b, p->stream));
     p->pending.push_back(pe);
     return r;
 }
@@ -501,11 +498,6 @@ int run_overflow_rows(nw_plan* p, int64_t c, void* dst, int out_kind) {
 constexpr int OUT_PSUM = 1001;    // internal run_chunk kinds: (ceil(c / 8), F, n) fp64 power partials,
 constexpr int OUT_PHSUM = 1002;   // complex fp64 phase partials (y / |y|)
 
-bool large_pipe() {
-    const char* e = std::getenv("NW_LARGE_PIPE");
-    return e && e[0] == '1';
-}
-
 int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
     // fused sizes: the forward R2C by nw_fused.hip's fwd_r2c_kernel (no copy, one kernel)
@@ -537,17 +529,9 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
             NW_HIP(nw::build_large_support(p->desc, p->dtype, p->d_wtab, p->stream));
             p->wtab_valid = true;
         }
-        const int64_t fc = nw::large_fchunk(p->n, p->nfreq, p->dtype);
-        // pipelined form (NW_LARGE_PIPE=1, A/B): the row pass of scale chunk k + 1 (main stream)
-        // beside the column pass of chunk k (second stream), B buffers alternating
-        const bool pipe = large_pipe() && p->nfreq > fc;
-        NW_TRY(ensure(&p->d_scratch, &p->d_scratch_bytes,
-                      nw::large_scratch_bytes(p->n, p->nfreq, p->dtype, pipe ? 2 : 1)));
-        if (pipe && !p->stream2) {
-            NW_HIP(hipStreamCreateWithFlags(&p->stream2, hipStreamNonBlocking));
-            for (auto& e : p->pipe_ev) NW_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
+        NW_TRY(ensure(&p->d_scratch, &p->d_scratch_bytes, nw::large_scratch_bytes(p->n, p->nfreq, p->dtype)));
         const size_t out_row = (size_t)p->n * (out_kind == NW_OUT_CWT ? 2 : 1) * p->esz;
+        const int64_t fc = nw::large_fchunk(p->n, p->nfreq, p->dtype);
         p->stats.kernel = NW_K_TWO_PASS;
         for (int64_t sidx = 0; sidx < c; ++sidx) {
             const char* Xs = (const char*)p->d_X + (size_t)sidx * p->nh * 2 * p->esz;
@@ -556,35 +540,16 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
                 NW_HIP(nw::large_transpose(p->desc, p->dtype, Xs, p->d_scratch, p->stream));
                 return NW_OK;
             }));
-            if (pipe) {
-                // the second stream starts after everything queued so far (inputs, transpose)
-                NW_HIP(hipEventRecord(p->pipe_ev[4], p->stream));
-                NW_HIP(hipStreamWaitEvent(p->stream2, p->pipe_ev[4], 0));
-            }
-            int k = 0;
-            for (int64_t f0 = 0; f0 < p->nfreq; f0 += fc, ++k) {
+            for (int64_t f0 = 0; f0 < p->nfreq; f0 += fc) {
                 const int nf = (int)std::min<int64_t>(fc, p->nfreq - f0);
-                const int bi = pipe ? (k & 1) : 0;
-                if (pipe && k >= 2) NW_HIP(hipStreamWaitEvent(p->stream, p->pipe_ev[2 + bi], 0));   // B[bi] read
                 NW_TRY(staged(p, ST_ROWS, [&] {
-                    NW_HIP(nw::large_rows_b(p->desc, p->dtype, (int)f0, nf, p->d_wtab, p->d_scratch, bi, p->stream));
+                    NW_HIP(nw::large_rows(p->desc, p->dtype, (int)f0, nf, p->d_wtab, p->d_scratch, p->stream));
                     return NW_OK;
                 }));
-                hipStream_t cs = p->stream;
-                if (pipe) {
-                    NW_HIP(hipEventRecord(p->pipe_ev[bi], p->stream));
-                    NW_HIP(hipStreamWaitEvent(p->stream2, p->pipe_ev[bi], 0));
-                    cs = p->stream2;
-                }
                 NW_TRY(staged(p, ST_FUSED, [&] {
-                    NW_HIP(nw::large_cols(p->desc, p->dtype, out_kind, (int)f0, nf, p->d_wtab, p->d_scratch, os, cs, bi));
+                    NW_HIP(nw::large_cols(p->desc, p->dtype, out_kind, (int)f0, nf, p->d_wtab, p->d_scratch, os, p->stream));
                     return NW_OK;
-                }, cs));
-                if (pipe) NW_HIP(hipEventRecord(p->pipe_ev[2 + bi], p->stream2));
-            }
-            if (pipe) {   // the main stream (and whatever follows on it) waits for the column passes
-                NW_HIP(hipEventRecord(p->pipe_ev[4], p->stream2));
-                NW_HIP(hipStreamWaitEvent(p->stream, p->pipe_ev[4], 0));
+                }));
             }
         }
         return NW_OK;
@@ -851,9 +816,6 @@ void free_plan(nw_plan* p) {
         if (p->pinned[i]) (void)hipHostFree(p->pinned[i]);
         if (p->pinned_ev[i]) (void)hipEventDestroy(p->pinned_ev[i]);
     }
-    for (auto e : p->pipe_ev)
-        if (e) (void)hipEventDestroy(e);
-    if (p->stream2) (void)hipStreamDestroy(p->stream2);
     if (p->own_stream) (void)hipStreamDestroy(p->own_stream);
     delete p;
 }

@@ -18,12 +18,6 @@ constexpr int kPackMax = 2;
 // smallest pass-0 variant: a W row's support is rounded up to it (1 and 2 add code without a
 // measurable gain)
 constexpr int kPruneMin = 4;
-// signal-pair kernel, real outputs: stage the last pass through LDS for 16-B stores (A/B switch)
-#ifdef NW_PAIR_STAGE
-constexpr bool kPairStage = true;
-#else
-constexpr bool kPairStage = false;
-#endif
 // fp32 kernels with E >= this take the next signal's X by LDS-DMA into the idle image before
 // the stores (E = 32: 1.99 -> 1.94 ms; E = 16: 0.362 -> 0.386 ms, so not there)
 constexpr int kXdmaMinE = 32;
@@ -907,41 +901,6 @@ __device__ __forceinline__ void passes_from(C2<T>* v, T* lds, int t, const C2<Sc
                     const int k = I::bfly(t, q) + bitrev<R>(i) * I::NS;
                     if (k <= N / 2) xr[k] = C2<S>{v[q * R + i].re, -v[q * R + i].im};
                 }
-        } else if constexpr (I::LAST && PAIRSIG && kPairStage && OUT != NW_OUT_CWT && !XD) {
-            // real outputs of the signal-pair kernel staged through the (idle) image: each lane
-            // writes its 2 x R values at their row positions (lane-consecutive, ds_write_b32),
-            // then reads back 16-B runs and stores them as 16-B global stores -- a quarter of
-            // the 4-B store instructions (NW_PAIR_STAGE A/B)
-            using O = typename OutT<OUT, S>::type;
-            static_assert(sizeof(O) == 4 && N * 2 * (int)sizeof(O) <= kImgElems<T, N, E> * (int)sizeof(T), "stage fits");
-            float* st = reinterpret_cast<float*>(lds);
-            lds_barrier();                         // every wave has read the image
-#pragma unroll
-            for (int q = 0; q < Q; ++q)
-#pragma unroll
-                for (int i = 0; i < R; ++i) {
-                    const int k = I::bfly(t, q) + bitrev<R>(i) * I::NS;
-                    const C2<T>& y = v[q * R + i];
-                    st[k] = out_value<OUT, S>(C2<S>{y.re.x, y.im.x});
-                    st[N + k] = out_value<OUT, S>(C2<S>{y.re.y, y.im.y});
-                }
-            lds_barrier();
-            using V4 = float __attribute__((ext_vector_type(4)));
-            constexpr int CH = N / 4 / Geometry<N, E>::T;          // 16-B chunks per lane per row
-#pragma unroll
-            for (int m = 0; m < CH; ++m) {
-                const int c = t + m * Geometry<N, E>::T;
-                const V4 a = *reinterpret_cast<const V4*>(st + 4 * c);
-                store_row<SP>(a, ocur, (uint32_t)t * 16u, (uint32_t)(m * Geometry<N, E>::T * 16));
-            }
-            if (ocur2) {
-#pragma unroll
-                for (int m = 0; m < CH; ++m) {
-                    const int c = t + m * Geometry<N, E>::T;
-                    const V4 b = *reinterpret_cast<const V4*>(st + N + 4 * c);
-                    store_row<SP>(b, ocur2, (uint32_t)t * 16u, (uint32_t)(m * Geometry<N, E>::T * 16));
-                }
-            }
         } else if constexpr (I::LAST) {
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (PAIRSIG) {

@@ -69,12 +69,10 @@ template <typename T> struct WLoad<T, false> {    // table wavelets: complex row
 // per launch; fp64 has no registers to spare (4 and 8 measured +-0 / slower, with spills);
 // n = 8192 (256-thread blocks) keeps 8: 16 spilled 12-16 B there
 constexpr int kWKeep32 = 16, kWKeep32Small = 8;
-// fp64 n = 16384 (A/B, NW_WKEEP64): the pass-1 twiddle table (Tab1) left 14 VGPRs of the 256
-#ifdef NW_WKEEP64
-constexpr int kWKeep64 = NW_WKEEP64;
-#else
-constexpr int kWKeep64 = 0;
-#endif
+// fp64 n = 16384: the pass-1 twiddle table (Tab1) left room for 8 W elements in the 256 VGPRs:
+// C4 shape fp64 8.21 -> 8.02 ms per launch (4: 8.10; 12 / 16 spill 28 / 52 B;
+// profiles/r05_f64_wkeep_ab.txt)
+constexpr int kWKeep64 = 8;
 // (W elements beyond kWKeep32 evaluated in registers for Morse rows instead of re-read:
 // C4 3.360-3.368 -> 3.420-3.430 ms per launch; removing those loads altogether (diagnostic)
 // 3.367-3.369: the re-read costs nothing, the evaluation's VALU does)

@@ -248,18 +248,13 @@ bool chirp_psum_ok(int dtype, bool phase, const int64_t* counts);
 // fp64.  scratch = Xt (n complex) + B (large_fchunk scales x n complex); support = kmax[nfreq]
 // + the fp64 column-pass twiddle tables.
 bool       large_supported(int64_t n, int dtype);
-// nb: B buffers (2 for the pipelined form: the row pass of one scale chunk beside the column
-// pass of the previous one on a second stream)
-size_t     large_scratch_bytes(int64_t n, int nfreq, int dtype, int nb = 1);
+size_t     large_scratch_bytes(int64_t n, int nfreq, int dtype);
 size_t     large_support_bytes(int nfreq);
 int64_t    large_fchunk(int64_t n, int nfreq, int dtype);
 hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStream_t s);
 hipError_t large_transpose(const WDesc& d, int dtype, const void* X, void* scratch, hipStream_t s);
 hipError_t large_rows(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, hipStream_t s);
 hipError_t large_cols(const WDesc& d, int dtype, int out_kind, int f0, int nf, const void* support,
-                      const void* scratch, void* out, hipStream_t s, int bi = 0);
-// B buffer bi of the scratch (rows write it, cols read it)
-hipError_t large_rows_b(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, int bi,
-                        hipStream_t s);
+                      const void* scratch, void* out, hipStream_t s);
 
 }  // namespace nw

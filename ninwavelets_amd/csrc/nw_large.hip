@@ -40,9 +40,6 @@
 // hits, the row pass loses its Xt reuse across the scales of a tile.
 #include <cstdlib>
 
-#ifdef NW_ROWS_TAB1   // A/B: the fp64 n2 = 16384 pass-1 twiddle table in the row pass too
-#define NW_TAB1_F64_16384 1
-#endif
 #include "nw_fft_dev.h"
 
 namespace nw {
@@ -352,15 +349,18 @@ template <typename T, int E, int KIND>
 constexpr bool kRowsXD = sizeof(T) == 4 && E >= 32 && KIND != NW_TABLE && !kRowsStream;
 // 4 waves/SIMD; fp64: 2 (twice the registers per element, as nw_fused)
 template <typename T, int N2, int E, int KIND>
-__device__ __forceinline__ void rows_block(int b, const WDesc& d, int f0, int nf, int n1, int rgs,
-                                           const C2<T>* __restrict__ Xt, C2<T>* __restrict__ B,
-                                           const int* __restrict__ kmax, const C2<T>* __restrict__ tw, T* lds) {
+__global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
+    WDesc d, int f0, int nf, int n1, int rgs, const C2<T>* __restrict__ Xt, C2<T>* __restrict__ B,
+    const int* __restrict__ kmax, const C2<T>* __restrict__ tw) {
     using G = Geometry<N2, E>;
+    extern __shared__ __align__(16) unsigned char smem[];
+    T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
 
     // XCD-aware block -> (scale, row group), as nw_fused_kernel: blocks b, b+8, ... share
     // an XCD, whose resident blocks cover kRowTileF scales x kRowTileG row groups, so each
     // Xt row group is read from HBM once per tile and then from that XCD's L2
+    const int b = blockIdx.x;
     const int xcd = b & 7;
     const int local = b >> 3;
     const int pos = local % (kRowTileF * kRowTileG);
@@ -493,21 +493,6 @@ __device__ __forceinline__ void rows_block(int b, const WDesc& d, int f0, int nf
     }
 }
 
-// nblk logical blocks over the grid (NW_ROWS_GRID caps the grid: the persistent form of the
-// pipelined two-pass A/B; by default grid = nblk, one iteration).  A block reusing its LDS for
-// the next logical block waits for every wave's last reads of the image first.
-template <typename T, int N2, int E, int KIND>
-__global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
-    WDesc d, int f0, int nf, int n1, int rgs, const C2<T>* __restrict__ Xt, C2<T>* __restrict__ B,
-    const int* __restrict__ kmax, const C2<T>* __restrict__ tw, int nblk) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    T* lds = reinterpret_cast<T*>(smem);
-    for (int b = blockIdx.x; b < nblk; b += gridDim.x) {
-        if (b != (int)blockIdx.x) lds_barrier();
-        rows_block<T, N2, E, KIND>(b, d, f0, nf, n1, rgs, Xt, B, kmax, tw, lds);
-    }
-}
-
 // ---- pass 2: columns.  Thread t owns column c = t % C of the workgroup's C columns and
 // butterflies u + q*U (U = N1/E threads per column).  The exchange image is
 // [position][column] (position-major, C reals per position), one real component at a
@@ -632,16 +617,19 @@ constexpr int kSplitLo = 4096;
 constexpr int kSplitEntries = 2 * kSplitLo;   // n <= 2^24: m >> 12 < 4096
 
 template <typename T, int N1, int N2, int OUT>
-__device__ __forceinline__ void cols_block(int bb, int f0, int nf, const C2<T>* __restrict__ B, void* __restrict__ out,
-                                           const C2<T>* __restrict__ tw1, const C2<T>* __restrict__ tsplit, T* lds) {
+__global__ __launch_bounds__(kColThreads<T>, sizeof(T) == 8 ? 2 : 4) void cols_kernel(
+    int f0, int nf, const C2<T>* __restrict__ B, void* __restrict__ out, const C2<T>* __restrict__ tw1,
+    const C2<T>* __restrict__ tsplit) {
     using CL = Cols<T, N1>;
     constexpr int C = CL::C, U = CL::U, E = CL::E;
     constexpr int64_t n = (int64_t)N1 * N2;
+    extern __shared__ __align__(16) unsigned char smem[];
+    T* lds = reinterpret_cast<T*>(smem);
     const int t = threadIdx.x;
     const int c = t % C, u = t / C;
     constexpr int ngroups = N2 / C;
-    const int fl = bb / ngroups;
-    const int cg = bb % ngroups;
+    const int fl = blockIdx.x / ngroups;
+    const int cg = blockIdx.x % ngroups;
     if (fl >= nf) return;
     const int col = cg * C + c;                      // n2
     // B[fl] (uniform base) + 32-bit lane offsets: (k1 * N2 + col) * 16 < n * 16 <= 2^28
@@ -693,17 +681,6 @@ __device__ __forceinline__ void cols_block(int bb, int f0, int nf, const C2<T>* 
     void* orow = reinterpret_cast<char*>(out) + (int64_t)(f0 + fl) * n * (int64_t)sizeof(O);
     const uint32_t ooff = ((uint32_t)col + (uint32_t)u * N2) * (uint32_t)sizeof(O);
     col_passes<T, N1, N2, OUT, 0>(v, lds, u, c, orow, ooff, tw1);
-}
-
-// nblk logical blocks over the grid (a grid smaller than nblk loops: the persistent form of
-// the pipelined two-pass A/B, NW_COLS_GRID; by default grid = nblk, one iteration)
-template <typename T, int N1, int N2, int OUT>
-__global__ __launch_bounds__(kColThreads<T>, sizeof(T) == 8 ? 2 : 4) void cols_kernel(
-    int f0, int nf, const C2<T>* __restrict__ B, void* __restrict__ out, const C2<T>* __restrict__ tw1,
-    const C2<T>* __restrict__ tsplit, int nblk) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    T* lds = reinterpret_cast<T*>(smem);
-    for (int bb = blockIdx.x; bb < nblk; bb += gridDim.x) cols_block<T, N1, N2, OUT>(bb, f0, nf, B, out, tw1, tsplit, lds);
 }
 
 // ---- fp32 column pass on column PAIRS: thread (cp, u) owns the adjacent columns 2cp, 2cp+1
@@ -807,16 +784,18 @@ __device__ __forceinline__ void colp_passes(C2<f2>* v, f2* lds, int u, int cp, v
 }
 
 template <int N1, int N2, int OUT>
-__device__ __forceinline__ void colp_block(int bb, int f0, int nf, const C2<float>* __restrict__ B, void* __restrict__ out,
-                                           f2* lds) {
+__global__ __launch_bounds__(ColsP<N1>::THREADS, ColsP<N1>::THREADS / 256) void cols_kernel(int f0, int nf, const C2<float>* __restrict__ B,
+                                                       void* __restrict__ out) {
     using CL = ColsP<N1>;
     constexpr int CP = CL::CP, C = CL::C, U = CL::U, E = CL::E;
     constexpr int64_t n = (int64_t)N1 * N2;
+    extern __shared__ __align__(16) unsigned char smem[];
+    f2* lds = reinterpret_cast<f2*>(smem);
     const int t = threadIdx.x;
     const int cp = t % CP, u = t / CP;
     constexpr int ngroups = N2 / C;
-    const int fl = bb / ngroups;
-    const int cg = bb % ngroups;
+    const int fl = blockIdx.x / ngroups;
+    const int cg = blockIdx.x % ngroups;
     if (fl >= nf) return;
     const int col = cg * C + 2 * cp;                 // n2 of the pair's first column
     const C2<float>* bf = B + (int64_t)fl * n;
@@ -849,14 +828,6 @@ __device__ __forceinline__ void colp_block(int bb, int f0, int nf, const C2<floa
     colp_passes<N1, N2, OUT, 0>(v, lds, u, cp, orow, ooff);
 }
 
-template <int N1, int N2, int OUT>
-__global__ __launch_bounds__(ColsP<N1>::THREADS, ColsP<N1>::THREADS / 256) void cols_kernel(int f0, int nf, const C2<float>* __restrict__ B,
-                                                       void* __restrict__ out, int nblk) {
-    extern __shared__ __align__(16) unsigned char smem[];
-    f2* lds = reinterpret_cast<f2*>(smem);
-    for (int bb = blockIdx.x; bb < nblk; bb += gridDim.x) colp_block<N1, N2, OUT>(bb, f0, nf, B, out, lds);
-}
-
 // tsplit for one n (fp64 column pass), from sincospi in fp64
 __global__ __launch_bounds__(256) void tsplit_kernel(C2<double>* ts, int64_t n) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -865,17 +836,6 @@ __global__ __launch_bounds__(256) void tsplit_kernel(C2<double>* ts, int64_t n) 
     double s, c;
     sincospi(2.0 * (double)(m % n) / (double)n, &s, &c);
     ts[i] = C2<double>{c, s};
-}
-
-// grid of a launch of `blocks` logical blocks: all of them, or at most the cap an environment
-// variable sets (a multiple of 8, so a block keeps its XCD class in the loop; A/B diagnostics)
-unsigned grid_cap(int64_t blocks, const char* env) {
-    int64_t g = blocks;
-    if (const char* e = std::getenv(env)) {
-        const int64_t c = std::atoll(e) / 8 * 8;
-        if (c > 0 && c < g) g = c;
-    }
-    return (unsigned)g;
 }
 
 template <typename T, int N2, int E, int KIND>
@@ -892,8 +852,8 @@ hipError_t launch_row_pass(const WDesc& d, int f0, int nf, int n1, const C2<T>* 
     const int gpad = (ngroups + 8 * kRowTileG - 1) / (8 * kRowTileG) * (8 * kRowTileG);
     const int nfr = (nf + kRowTileF - 1) / kRowTileF;
     const int64_t blocks = (int64_t)gpad * nfr * kRowTileF;
-    rows_kernel<T, N2, E, KIND><<<grid_cap(blocks, "NW_ROWS_GRID"), N2 / E, lds, s>>>(
-        d, f0, nf, n1, rgs, Xt, B, kmax, reinterpret_cast<const C2<T>*>(tw), (int)blocks);
+    rows_kernel<T, N2, E, KIND><<<(unsigned)blocks, N2 / E, lds, s>>>(d, f0, nf, n1, rgs, Xt, B, kmax,
+                                                                       reinterpret_cast<const C2<T>*>(tw));
     return hipGetLastError();
 }
 
@@ -911,13 +871,12 @@ hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, 
                                                     : (const void*)cols_kernel<N1, N2, NW_OUT_ABS>;
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
-        const unsigned g = grid_cap(blocks, "NW_COLS_GRID");
         if (out_kind == NW_OUT_CWT)
-            cols_kernel<N1, N2, NW_OUT_CWT><<<g, CL::THREADS, lds, s>>>(f0, nf, B, out, (int)blocks);
+            cols_kernel<N1, N2, NW_OUT_CWT><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
         else if (out_kind == NW_OUT_POWER)
-            cols_kernel<N1, N2, NW_OUT_POWER><<<g, CL::THREADS, lds, s>>>(f0, nf, B, out, (int)blocks);
+            cols_kernel<N1, N2, NW_OUT_POWER><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
         else
-            cols_kernel<N1, N2, NW_OUT_ABS><<<g, CL::THREADS, lds, s>>>(f0, nf, B, out, (int)blocks);
+            cols_kernel<N1, N2, NW_OUT_ABS><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
         return hipGetLastError();
     }
     using CL = Cols<T, N1>;
@@ -936,13 +895,12 @@ hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, 
                                                 : (const void*)cols_kernel<T, N1, N2, NW_OUT_ABS>;
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    const unsigned g = grid_cap(blocks, "NW_COLS_GRID");
     if (out_kind == NW_OUT_CWT)
-        cols_kernel<T, N1, N2, NW_OUT_CWT><<<g, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit, (int)blocks);
+        cols_kernel<T, N1, N2, NW_OUT_CWT><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     else if (out_kind == NW_OUT_POWER)
-        cols_kernel<T, N1, N2, NW_OUT_POWER><<<g, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit, (int)blocks);
+        cols_kernel<T, N1, N2, NW_OUT_POWER><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     else
-        cols_kernel<T, N1, N2, NW_OUT_ABS><<<g, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit, (int)blocks);
+        cols_kernel<T, N1, N2, NW_OUT_ABS><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
     return hipGetLastError();
 }
 
@@ -976,9 +934,9 @@ bool large_supported(int64_t n, int dtype) {
            !(n & (n - 1));
 }
 
-size_t large_scratch_bytes(int64_t n, int nfreq, int dtype, int nb) {
+size_t large_scratch_bytes(int64_t n, int nfreq, int dtype) {
     const size_t per = (size_t)n * cplx_bytes(dtype);
-    return per + (size_t)nb * (size_t)fchunk_of(n, nfreq, dtype) * per;   // Xt + nb x B
+    return per + (size_t)fchunk_of(n, nfreq, dtype) * per;   // Xt + B
 }
 
 size_t large_support_bytes(int nfreq) { return tsplit_offset(nfreq) + kSplitEntries * sizeof(C2<double>); }
@@ -1025,10 +983,10 @@ bool morse_fast_of(const WDesc& d) {
 }
 
 template <typename T>
-hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, hipStream_t s, int bi) {
+hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, hipStream_t s) {
     const Split sp = split_of(d.n, sizeof(T) == 4 ? NW_F32 : NW_F64);
     C2<T>* Xt = reinterpret_cast<C2<T>*>(scratch);
-    C2<T>* B = Xt + d.n + (int64_t)bi * fchunk_of(d.n, d.nfreq, sizeof(T) == 4 ? NW_F32 : NW_F64) * d.n;
+    C2<T>* B = Xt + d.n;
 #define NW_ROWS(NN)                                                                                          \
     case NN:                                                                                                 \
         if constexpr (NN <= kMaxN2<T>) {                                                                     \
@@ -1058,10 +1016,9 @@ hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, 
 
 template <typename T>
 hipError_t cols_t(const WDesc& d, int out_kind, int f0, int nf, const void* support, const void* scratch, void* out,
-                  hipStream_t s, int bi) {
+                  hipStream_t s) {
     const Split sp = split_of(d.n, sizeof(T) == 4 ? NW_F32 : NW_F64);
-    const C2<T>* B = reinterpret_cast<const C2<T>*>(scratch) + d.n +
-                     (int64_t)bi * fchunk_of(d.n, d.nfreq, sizeof(T) == 4 ? NW_F32 : NW_F64) * d.n;
+    const C2<T>* B = reinterpret_cast<const C2<T>*>(scratch) + d.n;
     const C2<T>* ts = sizeof(T) == 8 ? reinterpret_cast<const C2<T>*>(reinterpret_cast<const char*>(support) +
                                                                       tsplit_offset(d.nfreq))
                                      : nullptr;
@@ -1081,19 +1038,15 @@ hipError_t cols_t(const WDesc& d, int out_kind, int f0, int nf, const void* supp
 
 // pass 1 for scales [f0, f0 + nf): Xt -> B (both in the scratch)
 hipError_t large_rows(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, hipStream_t s) {
-    return large_rows_b(d, dtype, f0, nf, support, scratch, 0, s);
-}
-hipError_t large_rows_b(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, int bi,
-                        hipStream_t s) {
     const int* km = reinterpret_cast<const int*>(support);
-    return dtype == NW_F32 ? rows_t<float>(d, f0, nf, km, scratch, s, bi) : rows_t<double>(d, f0, nf, km, scratch, s, bi);
+    return dtype == NW_F32 ? rows_t<float>(d, f0, nf, km, scratch, s) : rows_t<double>(d, f0, nf, km, scratch, s);
 }
 
 // pass 2 for scales [f0, f0 + nf): B -> out rows (f, n) of one signal (out: its row 0)
 hipError_t large_cols(const WDesc& d, int dtype, int out_kind, int f0, int nf, const void* support,
-                      const void* scratch, void* out, hipStream_t s, int bi) {
-    return dtype == NW_F32 ? cols_t<float>(d, out_kind, f0, nf, support, scratch, out, s, bi)
-                           : cols_t<double>(d, out_kind, f0, nf, support, scratch, out, s, bi);
+                      const void* scratch, void* out, hipStream_t s) {
+    return dtype == NW_F32 ? cols_t<float>(d, out_kind, f0, nf, support, scratch, out, s)
+                           : cols_t<double>(d, out_kind, f0, nf, support, scratch, out, s);
 }
 
 }  // namespace nw
