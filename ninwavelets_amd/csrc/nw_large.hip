@@ -334,7 +334,8 @@ template <int KIND> struct RowW<double, KIND> {
 // ---- pass 1: rows
 // fp32 E = 32 rows: pruned Xt rows by LDS-DMA ahead of the stores (C5 50.6 -> 48.5 ms per step);
 // analytic kinds only (table rows' wavelet_bin loads would exceed 128 VGPRs, as in nw_fused);
-// fp64 rows with the same DMA measured no faster (0.94 -> 0.98 ms per launch)
+// fp64 rows with the same DMA measured no faster (0.94 -> 0.98 ms per launch; round 5, after the
+// W-evaluator changes: rows -0.5 %, step +1.4 %, profiles/r05_c5f64_rows_xd_ab.txt)
 // (fp64 rows with the DMA, re-measured in round 4 beside the fast Morse form: no gain either,
 // profiles/r04_c5f64_rows_ab.txt)
 // NW_ABL_ROWS_STREAM (diagnostic, wrong results): the row pass as a pure stream -- the pass-0
