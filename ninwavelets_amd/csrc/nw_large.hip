@@ -120,6 +120,14 @@ constexpr int kMorseFast35 = 102;
 // (WDesc::morse_ovf): the overflow-checked form (its own instantiation, so the default rows
 // carry no check)
 constexpr int kMorseOvf = 101;
+// ... and b = 17.5 rows that start at bin 0 (WDesc::off == 0: every bin of a row is >= 0) with
+// the exponential factor by a product recurrence over the thread's bins (RowW<double>::Rec)
+constexpr int kMorseRec = 103;
+#ifdef NW_ROWS_NO_REC   // diagnostic A/B: the per-bin exp form (kMorseFast35) for every b = 17.5 row
+constexpr bool kRowsRec = false;
+#else
+constexpr bool kRowsRec = true;
+#endif
 template <int KIND> struct RowW<float, KIND> {
     float xs, b, c1, rr, cpi, sigma, kappa, scale;
     int off, lenv, jlim;
@@ -231,7 +239,7 @@ __device__ __forceinline__ double exp_rows(double y, const ExpK& K) {
 }
 
 template <int KIND> struct RowW<double, KIND> {
-    static constexpr bool MORSE = KIND == NW_MORSE || KIND == kMorseFast || KIND == kMorseFast35;
+    static constexpr bool MORSE = KIND == NW_MORSE || KIND == kMorseFast || KIND == kMorseFast35 || KIND == kMorseRec;
     // kMorseFast: x^b by a multiply chain (+ one sqrt for the half) and x^3 by two multiplies,
     // then ONE exp -- 2 x^b exp((b/r)(1 - x^3)), the reference's own factorisation
     // (wavelets.py:65-74) -- instead of one log and two exps.  kMorseFast35 (b = 17.5, round 5)
@@ -240,8 +248,9 @@ template <int KIND> struct RowW<double, KIND> {
     // around each one were s_and_saveexec / s_cbranch pairs that serialised them), with the
     // sqrt without the compiler's denormal scaling and class checks (x >= delta / f is normal
     // for every valid bin)
-    static constexpr bool FAST = KIND == kMorseFast || KIND == kMorseFast35;
+    static constexpr bool FAST = KIND == kMorseFast || KIND == kMorseFast35 || KIND == kMorseRec;
     double delta, f, xs, peak, b, r, bor, sigma, cpi, kappa, scale, scale2;
+    double dx, dd;                                           // kMorseRec: bin stride in x, e^(third difference)
     int off, lenv;
     int bint, bhalf, jm1;
     ExpK ek;
@@ -284,8 +293,39 @@ template <int KIND> struct RowW<double, KIND> {
         d = fma(-s, s, x);
         return fma(d, h, s);
     }
+    // kMorseRec: the exponential factor e^{E(x)}, E(x) = (b/r)(1 - x^3), over a thread's bins
+    // x_g + i D (D = the bin stride times xs) by products of its finite differences: E is a
+    // cubic, so e^{E(x+D)} = e^{E(x)} a, a <- a c, c <- c dd with a = e^{E(x+D) - E(x)},
+    // c = e^{second difference} and dd = e^{-6 (b/r) D^3} constant per scale -- three
+    // multiplies per bin instead of an exp.  Restarted with three exps every kRecGroup bins:
+    // the rounding of c and dd is raised to the C(i,2) / C(i,3) power within a group, so 16
+    // keeps psi within 3.3e-14 of its row maximum (numpy emulation against long double over
+    // D = 0.004 .. 10; the direct exp: 1e-15), far inside the 1e-12 parity contract
+    static constexpr int kRecGroup = 16;
+    struct Rec { double e, a, c; };
+    __device__ __forceinline__ void init_rec(int stride) {
+        dx = pin((double)stride * xs);
+        dd = pin(exp_rows<true>(-bor * (6.0 * (dx * dx * dx)), ek));
+    }
+    __device__ __forceinline__ Rec start(int j) const {
+        const double x = (double)j * xs;
+        const double e0 = bor * (1.0 - (x * x) * x);
+        const double d1 = -bor * (dx * (3.0 * (x * x) + dx * (3.0 * x + dx)));   // E(x + D) - E(x)
+        const double d2 = -bor * (6.0 * (dx * dx) * (x + dx));                  // its difference
+        return Rec{exp_rows<true>(e0, ek), exp_rows<true>(d1, ek), exp_rows<true>(d2, ek)};
+    }
+    __device__ __forceinline__ double step(int j, Rec& q) const {
+        const double x = (double)j * xs;
+        const double x2 = x * x, x4 = x2 * x2, x8 = x4 * x4, x16 = x8 * x8;
+        const double xb = (x16 * x) * sqrt_normal(x);
+        const double psi = (xb * q.e) * scale2;
+        q.e *= q.a;
+        q.a *= q.c;
+        q.c *= dd;
+        return (unsigned)(j - 1) < (unsigned)jm1 ? psi : 0.0;
+    }
     __device__ __forceinline__ double operator()(int j) const {
-        if constexpr (KIND == kMorseFast35) {
+        if constexpr (KIND == kMorseFast35 || KIND == kMorseRec) {
             // branch-free (the general kMorseFast form below keeps its branches: interleaved,
             // its runtime chain and sqrt select spilled 236 B)
             const double x = (double)j * xs;
@@ -330,6 +370,10 @@ template <int KIND> struct RowW<double, KIND> {
         return psi * scale;
     }
 };
+
+// the recurrence state of a row's W evaluation (kMorseRec), or nothing
+template <typename T, int KIND> struct RowRec { struct type {}; };
+template <> struct RowRec<double, kMorseRec> { using type = RowW<double, kMorseRec>::Rec; };
 
 // ---- pass 1: rows
 // fp32 E = 32 rows: pruned Xt rows by LDS-DMA ahead of the stores (C5 50.6 -> 48.5 ms per step);
@@ -376,6 +420,7 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
     NW_DCHECK(fi < d.nfreq && (rg + 1) * rgs <= n1 && (int64_t)n1 * N2 == d.n && km < d.n);
     RowW<T, KIND> wf;
     if constexpr (KIND != NW_TABLE) wf.init(d, fi);
+    if constexpr (sizeof(T) == 8 && KIND == kMorseRec) wf.init_rec(n1 * G::T);
 
     Tab1<T, N2, E>::fill(lds, tw, t);
     TwSplit<T, N2, E>::fill(lds, tw, t);
@@ -423,6 +468,7 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
             int tl = t;                            // opaque here: LDS reads must not hoist above the dispatch
             asm volatile("" : "+v"(tl));
             const C2<T>* xl = reinterpret_cast<const C2<T>*>(lds);
+            [[maybe_unused]] typename RowRec<T, KIND>::type rec{};
 #pragma unroll
             for (int r = 0; r < E; ++r) {
                 if (r < NZ) {
@@ -430,7 +476,12 @@ __global__ __launch_bounds__(N2 / E, sizeof(T) == 8 ? 2 : 4) void rows_kernel(
                     if constexpr (FROM_LDS) xv = xl[tl + r * G::T];
                     else xv = *at(xrow, xo, (uint32_t)(r * G::T * sizeof(C2<T>)));
                     const int j = j0 + r * n1 * G::T;
-                    if constexpr (KIND == NW_TABLE) {
+                    if constexpr (sizeof(T) == 8 && KIND == kMorseRec) {
+                        if (r % RowW<T, KIND>::kRecGroup == 0) rec = wf.start(j);
+                        const T w = wf.step(j, rec);
+                        v[r] = C2<T>{w * xv.re, w * xv.im};
+                        if (r % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+                    } else if constexpr (KIND == NW_TABLE) {
                         const cplx<T> w = wavelet_bin<T>(d, fi, (int64_t)j);
                         v[r] = cmul(C2<T>{w.re, w.im}, xv);
                     } else {
@@ -996,7 +1047,8 @@ hipError_t rows_t(const WDesc& d, int f0, int nf, const int* km, void* scratch, 
                 case NW_MORSE:                                                                               \
                     if constexpr (sizeof(T) == 8)                                                            \
                         if (morse_fast_of(d))                                                                \
-                            return d.b == 17.5 ? launch_row_pass<T, NN, EE, kMorseFast35>(d, f0, nf, sp.n1, Xt, B, km, s) \
+                            return d.b == 17.5 ? (kRowsRec && d.off == 0 ? launch_row_pass<T, NN, EE, kMorseRec>(d, f0, nf, sp.n1, Xt, B, km, s) \
+                                                             : launch_row_pass<T, NN, EE, kMorseFast35>(d, f0, nf, sp.n1, Xt, B, km, s)) \
                                                : launch_row_pass<T, NN, EE, kMorseFast>(d, f0, nf, sp.n1, Xt, B, km, s);  \
                     if constexpr (sizeof(T) == 4)                                                            \
                         if (d.morse_ovf) return launch_row_pass<T, NN, EE, kMorseOvf>(d, f0, nf, sp.n1, Xt, B, km, s); \

@@ -243,3 +243,34 @@ def test_morse_overflow_rows_fp32(n):
             assert np.isnan(got[f]).all(), freqs[f]
         else:
             assert rel_err(got[f], ref[f]) <= tol(n), freqs[f]
+
+
+@pytest.mark.parametrize('grid', ['full', 'half'])
+def test_large_fp64_morse_rows_each_scale(grid):
+    """The fp64 b = 17.5 row pass's two evaluators, every row on its own scale: rows that
+    start at bin 0 (the plan's grid spans n: WDesc::off = 0) take the exponential factor by
+    the product recurrence of nw_large.hip RowW<double>::Rec, rows of a shorter grid
+    (real_length n / 2: pad_to centres them, off = n / 4) the per-bin exp.  24 scales from
+    C5's range (bin strides in x from ~0.1 to ~70) against y = ifft(pad_to(W) * fft(x)) of
+    the oracle's rows; 1e-12 of each row's own max (the parity contract is per signal)."""
+    torch = pytest.importorskip('torch')
+    from ninwavelets_amd import _lib as L
+    n = 1 << 20
+    freqs = np.linspace(0.5, 250, 24)
+    rl = n / 1000. if grid == 'full' else n / 2000.
+    x = synth(1, n, seed=5)[0].astype(np.float64)
+    p = nw.Plan(n, freqs.size, 'float64', max_batch=1)
+    p.set_wavelet('morse', [17.5, 3.0], freqs, L.trans_grid(rl, 1000., False))
+    xt = torch.from_numpy(x[None]).cuda()
+    ot = torch.empty((1, freqs.size, n), dtype=torch.complex128, device='cuda')
+    p.execute(xt, ot, out_kind='cwt')
+    p.sync()
+    st = p.stats()
+    assert st['engine'] == 'fused' and st['launches_rows'] > 0, st
+    got = ot[0].cpu().numpy()
+    p.close()
+    rows = O.fft_wavelets('morse', freqs, 1000., rl, False)
+    assert (rows[0].shape[0] == n) == (grid == 'full')
+    ref = O.cwt_from_rows(x, rows, False)
+    for f in range(freqs.size):
+        assert rel_err(got[f], ref[f]) <= 1e-12, (grid, freqs[f], rel_err(got[f], ref[f]))
