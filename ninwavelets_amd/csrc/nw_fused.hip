@@ -73,6 +73,8 @@ constexpr int kWKeep32 = 16, kWKeep32Small = 8;
 // C4 shape fp64 8.21 -> 8.02 ms per launch (4: 8.10; 12 / 16 spill 28 / 52 B;
 // profiles/r05_f64_wkeep_ab.txt)
 constexpr int kWKeep64 = 8;
+// the pair kernel (E = 16): W elements kept in registers for the block (nw_fused_pair_kernel)
+constexpr int kPairWKeep = 12;
 // (W elements beyond kWKeep32 evaluated in registers for Morse rows instead of re-read:
 // C4 3.360-3.368 -> 3.420-3.430 ms per launch; removing those loads altogether (diagnostic)
 // 3.367-3.369: the re-read costs nothing, the evaluation's VALU does)
@@ -344,9 +346,14 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
 
     const float* wrow = reinterpret_cast<const float*>(wtab) + (int64_t)fi * N;
     const uint32_t wo = (uint32_t)t * (uint32_t)sizeof(float);
-    float w[E];
+    // the block's W elements r < kPairWKeep in registers; the rest (read only by the NZ = E
+    // pass 0: analytic rows end at the Nyquist bin, r <= E/2) re-read from L2 there.  All E
+    // kept spilled 4 of them (16-24 B of scratch at 128 VGPRs) in the |y| / |y|^2 kernels
+    constexpr int WK = kPairWKeep < E ? kPairWKeep : E;
+    float w[WK];
 #pragma unroll
-    for (int r = 0; r < E; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(float)));
+    for (int r = 0; r < WK; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(float)));
+    auto w_at = [&](int r) { return r < WK ? w[r < WK ? r : 0] : *at(wrow, wo, (uint32_t)(r * G::T * sizeof(float))); };
     Tab1<f2, N, E>::fill(lds, tw, t);
     const int64_t out_esz = (int64_t)(OUT == NW_OUT_CWT ? sizeof(C2<float>) : sizeof(float));
     const int nz = wnz[fi];
@@ -420,9 +427,14 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
                 load_x<float, N, E, NZ>(xb, xrow(s2), t);
             }
 #pragma unroll
-            for (int r = 0; r < E; ++r)
-                v[r] = r < NZ ? C2<f2>{f2{w[r] * xa[r].re, w[r] * xb[r].re}, f2{w[r] * xa[r].im, w[r] * xb[r].im}}
-                              : C2<f2>{f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
+            for (int r = 0; r < E; ++r) {
+                if (r < NZ) {
+                    const float wr = w_at(r);
+                    v[r] = C2<f2>{f2{wr * xa[r].re, wr * xb[r].re}, f2{wr * xa[r].im, wr * xb[r].im}};
+                } else {
+                    v[r] = C2<f2>{f2{0.0f, 0.0f}, f2{0.0f, 0.0f}};
+                }
+            }
             idft_br<f2, E, NZ>(v);
         };
         if (nz <= 4) pass0.template operator()<4>();
