@@ -240,14 +240,28 @@ template <int N, int E> struct Geometry {
     }
 };
 
-// The image feeding pass P and its padding group (2 pad slots per kPadG<E> slots).  (A
-// per-16 padding of the signal-pair kernel's 0 -> 1 image at n = 4096 removed its 2-way
-// pass-0 write conflicts, 0.54 of LDS cycles at C3, but measured 1.4 % slower: not kept.)
+// The image feeding pass P and its padding group (2 pad slots per kPadG<E> slots, or per 16
+// for the signal-pair kernel's 0 -> 1 image at n = 4096: kPad16 below).
 template <int PG> __device__ __forceinline__ int lds_idx_p(int i) { return i + 2 * (i / PG); }
 template <int PG> constexpr int lds_off_p(int c) { return c + 2 * (c / PG); }
 template <typename T> constexpr bool kIsPair = !std::is_same<T, Sc<T>>::value;
-template <typename T, int N, int E, int P> constexpr int kPadX = kPadG<E>;
-template <typename T, int N, int E> constexpr int kImgElems = lds_elems<N, E>();
+// Signal-pair kernel at T = 256 (n = 4096, E = 16): pass 0 writes each lane's 16 slots as
+// 8 ds_write_b128; with 2 pad slots per 32 two lanes share a pad block, so lanes t, t+1 of
+// every 8-lane group hit the same banks (2-way on every pass-0 write).  kPad16 pads the
+// 0 -> 1 image per 16 slots (stride 18 slots = 36 dwords per lane: conflict-free writes), and
+// pass 1's lanes 16-31 of each 32-lane ds_read_b64 group take the butterfly block 8 blocks
+// further (PassInfo::REMAP: 8 * 18 slots = 288 = 32 mod 64 dwords), so those reads stay
+// conflict-free too.  The 1 -> 2 image keeps 2 per 32 (its accesses are lane-contiguous).
+// Measured: round 2, 1.4 % slower (the layout pushed the power kernel from 16 to 20 B of
+// scratch); round 5, with the pair kernels at 0 B of scratch, C3 1.1258 -> 1.1156 ms per
+// launch (-0.9 %, profiles/r05_c3_pad16_ab.txt).  -DNW_PAIR_PAD16=0: the per-32 image.
+#ifndef NW_PAIR_PAD16
+#define NW_PAIR_PAD16 1
+#endif
+template <typename T, int N, int E>
+constexpr bool kPad16 = NW_PAIR_PAD16 && kIsPair<T> && E == 16 && N / E == 256 && Geometry<N, E>::npass() > 2;
+template <typename T, int N, int E, int P> constexpr int kPadX = (kPad16<T, N, E> && P == 1) ? 16 : kPadG<E>;
+template <typename T, int N, int E> constexpr int kImgElems = kPad16<T, N, E> ? N + 2 * (N / 16) : lds_elems<N, E>();
 
 // output value of one point: y, |y| or |y|^2
 template <int OUT, typename T> struct OutT { using type = T; };
@@ -438,8 +452,11 @@ template <int N, int E, int P, int OSZ, bool PK> struct PassInfo {
     // 544 = 32 mod 64 dwords), so a group covers the 64 banks once.  Stores stay whole:
     // each store instruction writes two 512-B runs.
     static constexpr bool SWZ = PAIRED && G::T == 512 && kPadG<E> == 32;
+    // the signal-pair kernel's pass 1 reads the per-16-padded image (kPad16)
+    static constexpr bool REMAP = PK && NW_PAIR_PAD16 && P == 1 && !LAST && E == 16 && G::T == 256 && Q == 1;
     __device__ static __forceinline__ int bfly(int t, int q) {
         if constexpr (SWZ) return 2 * (((t >> 5) << 4) + (((t >> 4) & 1) << 8) + (t & 15)) + q;
+        if constexpr (REMAP) return ((t >> 5) << 4) + (((t >> 4) & 1) << 7) + (t & 15);
         return PAIRED ? Q * t + q : t + q * G::T;
     }
 };

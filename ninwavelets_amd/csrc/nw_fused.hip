@@ -75,6 +75,8 @@ constexpr int kWKeep32 = 16, kWKeep32Small = 8;
 constexpr int kWKeep64 = 8;
 // the pair kernel (E = 16): W elements kept in registers for the block (nw_fused_pair_kernel)
 constexpr int kPairWKeep = 12;
+// ... in the |y| and power-partial pair kernels (their sqrt / fp64 accumulators take the registers)
+constexpr int kPairWKeepRed = 10;
 // (W elements beyond kWKeep32 evaluated in registers for Morse rows instead of re-read:
 // C4 3.360-3.368 -> 3.420-3.430 ms per launch; removing those loads altogether (diagnostic)
 // 3.367-3.369: the re-read costs nothing, the evaluation's VALU does)
@@ -349,7 +351,8 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
     // the block's W elements r < kPairWKeep in registers; the rest (read only by the NZ = E
     // pass 0: analytic rows end at the Nyquist bin, r <= E/2) re-read from L2 there.  All E
     // kept spilled 4 of them (16-24 B of scratch at 128 VGPRs) in the |y| / |y|^2 kernels
-    constexpr int WK = kPairWKeep < E ? kPairWKeep : E;
+    constexpr int WK = (OUT == NW_OUT_CWT || OUT == NW_OUT_POWER ? kPairWKeep : kPairWKeepRed) < E
+                           ? (OUT == NW_OUT_CWT || OUT == NW_OUT_POWER ? kPairWKeep : kPairWKeepRed) : E;
     float w[WK];
 #pragma unroll
     for (int r = 0; r < WK; ++r) w[r] = *at(wrow, wo, (uint32_t)(r * G::T * sizeof(float)));

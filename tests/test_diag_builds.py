@@ -14,9 +14,11 @@ from conftest import ROOT
 HIPCC = '/opt/rocm/bin/hipcc'
 CSRC = os.path.join(ROOT, 'ninwavelets_amd', 'csrc')
 SWITCHES = {
-    'nw_fused.hip': ['NW_ABL_NOWLOAD', 'NW_STAMPS', 'NW_ABL_NOSTORE', 'NW_ABL_NOTWIDDLE', 'NW_ABL_NOEXCH'],
+    'nw_fused.hip': ['NW_ABL_NOWLOAD', 'NW_STAMPS', 'NW_ABL_NOSTORE', 'NW_ABL_NOTWIDDLE', 'NW_ABL_NOEXCH',
+                     'NW_PAIR_PAD16=0'],
     'nw_large.hip': ['NW_ABL_ROWS_NOW', 'NW_B_PLAIN', 'NW_ABL_COLS_NOFFT', 'NW_ABL_COLS_NOSTORE',
-                     'NW_ABL_COLS_NOTW', 'NW_ABL_COLS_STREAM', 'NW_ABL_ROWS_STREAM', 'NW_ABL_NOSTORE', 'NW_ABL_NOTWIDDLE', 'NW_ABL_NOEXCH'],
+                     'NW_ABL_COLS_NOTW', 'NW_ABL_COLS_STREAM', 'NW_ABL_ROWS_STREAM', 'NW_ABL_NOSTORE', 'NW_ABL_NOTWIDDLE', 'NW_ABL_NOEXCH',
+                     'NW_ROWS_NO_REC'],
 }
 
 
