@@ -513,25 +513,35 @@ __global__ __launch_bounds__(256) void wtable_kernel(WDesc d, void* wtab) {
 }
 
 // Support of each W row for pass-0 pruning: wnz[f] >= the number of pass-0 elements r
-// (bins k = t + r*T, t < T) reaching the row's last nonzero bin, i.e. elements r >= wnz[f]
-// see W = 0 exactly for every thread: the next power of two up to 4, then the next multiple
+// (bins k = t + r*T, t < T) reaching the row's last bin above kTailRel x its max, i.e. elements
+// r >= wnz[f] see only the row's negligible tail for every thread (they run as zeros): the
+// next power of two up to 4, then the next multiple
 // of 4 (the pass-0 variants: NZ = 4, 8, 12, 16 at E = 16; 4, 8, 12, 16, 20, 24, 32 at E = 32
 // fp32; a multiple of 2^WSH, so nz >> WSH is exact for the partial-sum kernels' smaller E).
 // Rows pruned in steps of 4 elements: C3 1.205 -> 1.186 ms per launch (NZ = 12 at E = 16).
+// The support ends at the last bin above kTailRel x the row's max |W| (nw_internal.h).
 template <typename T, bool REALW>
 __global__ __launch_bounds__(256) void wsupport_kernel(const void* wtab, int64_t n, int tt, int e, int* wnz) {
     __shared__ int kmax[256];
+    __shared__ T wmax[256];
     const int fi = blockIdx.x;
-    int m = -1;
-    for (int64_t k = threadIdx.x; k < n; k += 256) {
-        bool nzv;
-        if constexpr (REALW) nzv = reinterpret_cast<const T*>(wtab)[(int64_t)fi * n + k] != T(0);
-        else {
-            const C2<T> w = reinterpret_cast<const C2<T>*>(wtab)[(int64_t)fi * n + k];
-            nzv = w.re != T(0) || w.im != T(0);
-        }
-        if (nzv) m = (int)k;
+    auto mag = [&](int64_t k) -> T {
+        if constexpr (REALW) return fabs(reinterpret_cast<const T*>(wtab)[(int64_t)fi * n + k]);
+        const C2<T> w = reinterpret_cast<const C2<T>*>(wtab)[(int64_t)fi * n + k];
+        return fmax(fabs(w.re), fabs(w.im));
+    };
+    T mx = T(0);
+    for (int64_t k = threadIdx.x; k < n; k += 256) mx = fmax(mx, (T)tail_max_term((double)mag(k)));
+    wmax[threadIdx.x] = mx;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) wmax[threadIdx.x] = fmax(wmax[threadIdx.x], wmax[threadIdx.x + w]);
+        __syncthreads();
     }
+    const double thr = kTailRel<T> * (double)wmax[0];
+    int m = -1;
+    for (int64_t k = threadIdx.x; k < n; k += 256)
+        if (tail_in_support((double)mag(k), thr)) m = (int)k;
     kmax[threadIdx.x] = m;
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {

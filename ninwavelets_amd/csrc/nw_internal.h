@@ -223,6 +223,21 @@ hipError_t fused_twiddles(int64_t n, int dtype, void** out);   // exact exp(+2 p
 // chirp-z kernel (kGroupC), each static_assert'ed equal to it, so one fused_psum_groups sizes
 // and accumulates the partial rows of either form
 constexpr int kPsumGroup = 8;
+
+// W support for the pruned pass 0 / row pass (wsupport_kernel, kmax_kernel): the last bin
+// whose |W| exceeds kTailRel x the row's max |W|.  The bins past it (the far tail of a Morse
+// row, exactly zero only where exp underflows, ~9x the peak frequency in fp64) are left out;
+// each holds |W| below kTailRel of the row's peak, so together they move y by less than
+// n * kTailRel of the signal's scale: 2^-48 (fp64) / 2^-32 (fp32) at n = 2^24, far below each
+// dtype's own FFT rounding (1e-15 / 1e-7) and the parity contract (1e-12 / 1e-5).  Non-finite
+// bins (the reference's inf / NaN rows, morse_special) stay in the support and out of the max.
+#ifdef NW_TAIL_EXACT   // diagnostic A/B: the exact support (every nonzero bin)
+template <typename T> constexpr double kTailRel = 0.0;
+#else
+template <typename T> constexpr double kTailRel = sizeof(T) == 8 ? 0x1p-72 : 0x1p-56;
+#endif
+__host__ __device__ inline double tail_max_term(double mag) { return mag <= 1.7976931348623157e308 ? mag : 0.0; }
+__host__ __device__ inline bool tail_in_support(double mag, double thr) { return !(mag <= thr); }
 bool fused_psum_supported(int64_t n, int dtype, int kind, bool phase);
 int64_t fused_psum_groups(int64_t nsig);
 int fused_psum_kernel_id(int64_t n, int dtype, bool phase);   // NW_K_FUSED or NW_K_FUSED_PAIR

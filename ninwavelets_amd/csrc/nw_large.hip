@@ -85,19 +85,40 @@ __global__ __launch_bounds__(256) void xt_kernel(WDesc d, const cplx<T>* __restr
     for (int i = ty; i < 32; i += 8) Xt[(int64_t)(k1_0 + i) * n2 + k2_0 + tx] = tile[tx][i];
 }
 
-// ---- kmax[f] = last bin k < min(n, xlim) with W_f[k] != 0 (-1: none); pass-1 pruning
+// ---- kmax[f] = last bin k < min(n, xlim) with |W_f[k]| above kTailRel x the row's max |W|
+// (nw_internal.h; -1: none); pass-1 pruning.  wmax_kernel first: the row maxima as the bit
+// patterns of non-negative doubles (ordered as unsigned integers, so atomicMax keeps the max)
 constexpr int kSupBins = 16;   // bins per thread
 template <typename T, bool REALW>
-__global__ __launch_bounds__(256) void kmax_kernel(WDesc d, int* __restrict__ kmax) {
+__device__ __forceinline__ double wmag(const WDesc& d, int fi, int64_t k) {
+    const cplx<T> w = wavelet_bin<T>(d, fi, k);
+    return REALW ? fabs((double)w.re) : fmax(fabs((double)w.re), fabs((double)w.im));
+}
+template <typename T, bool REALW>
+__global__ __launch_bounds__(256) void wmax_kernel(WDesc d, unsigned long long* __restrict__ wmax) {
     const int fi = blockIdx.y;
     const int64_t lim = d.xlim < d.n ? d.xlim : d.n;
     const int64_t k0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kSupBins;
+    double m = 0.0;
+    for (int i = 0; i < kSupBins; ++i) {
+        const int64_t k = k0 + i;
+        if (k >= lim) break;
+        m = fmax(m, tail_max_term(wmag<T, REALW>(d, fi, k)));
+    }
+    for (int o = 32; o > 0; o >>= 1) m = fmax(m, __shfl_xor(m, o, 64));
+    if ((threadIdx.x & 63) == 0 && m > 0.0) atomicMax(&wmax[fi], (unsigned long long)__double_as_longlong(m));
+}
+template <typename T, bool REALW>
+__global__ __launch_bounds__(256) void kmax_kernel(WDesc d, int* __restrict__ kmax, const unsigned long long* __restrict__ wmax) {
+    const int fi = blockIdx.y;
+    const int64_t lim = d.xlim < d.n ? d.xlim : d.n;
+    const int64_t k0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * kSupBins;
+    const double thr = kTailRel<T> * __longlong_as_double((long long)wmax[fi]);
     int m = -1;
     for (int i = 0; i < kSupBins; ++i) {
         const int64_t k = k0 + i;
         if (k >= lim) break;
-        const cplx<T> w = wavelet_bin<T>(d, fi, k);
-        if (w.re != T(0) || (!REALW && w.im != T(0))) m = (int)k;
+        if (tail_in_support(wmag<T, REALW>(d, fi, k), thr)) m = (int)k;
     }
     // wave max, then one atomic per wave
     for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o, 64));
@@ -977,7 +998,9 @@ int64_t fchunk_of(int64_t n, int nfreq, int dtype) {
 }
 
 // support buffer: kmax[nfreq] (padded to 256 B), then the fp64 split twiddles
-size_t tsplit_offset(int nfreq) { return ((size_t)nfreq * sizeof(int) + 255) / 256 * 256; }
+// support buffer: kmax (int) | row maxima (u64) | tsplit (fp64)
+size_t wmax_offset(int nfreq) { return ((size_t)nfreq * sizeof(int) + 255) / 256 * 256; }
+size_t tsplit_offset(int nfreq) { return wmax_offset(nfreq) + ((size_t)nfreq * sizeof(uint64_t) + 255) / 256 * 256; }
 
 }  // namespace
 
@@ -995,17 +1018,24 @@ size_t large_support_bytes(int nfreq) { return tsplit_offset(nfreq) + kSplitEntr
 
 hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStream_t s) {
     int* kmax = reinterpret_cast<int*>(support);
+    auto* wmax = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(support) + wmax_offset(d.nfreq));
     hipError_t e = hipMemsetAsync(kmax, 0xFF, (size_t)d.nfreq * sizeof(int), s);   // -1
+    if (e != hipSuccess) return e;
+    e = hipMemsetAsync(wmax, 0, (size_t)d.nfreq * sizeof(uint64_t), s);            // +0.0
     if (e != hipSuccess) return e;
     const int64_t per_block = 256 * kSupBins;
     dim3 grid((unsigned)((d.n + per_block - 1) / per_block), (unsigned)d.nfreq);
     const bool realw = d.kind != NW_TABLE;
     if (dtype == NW_F32) {
-        if (realw) kmax_kernel<float, true><<<grid, 256, 0, s>>>(d, kmax);
-        else kmax_kernel<float, false><<<grid, 256, 0, s>>>(d, kmax);
+        if (realw) wmax_kernel<float, true><<<grid, 256, 0, s>>>(d, wmax);
+        else wmax_kernel<float, false><<<grid, 256, 0, s>>>(d, wmax);
+        if (realw) kmax_kernel<float, true><<<grid, 256, 0, s>>>(d, kmax, wmax);
+        else kmax_kernel<float, false><<<grid, 256, 0, s>>>(d, kmax, wmax);
     } else {
-        if (realw) kmax_kernel<double, true><<<grid, 256, 0, s>>>(d, kmax);
-        else kmax_kernel<double, false><<<grid, 256, 0, s>>>(d, kmax);
+        if (realw) wmax_kernel<double, true><<<grid, 256, 0, s>>>(d, wmax);
+        else wmax_kernel<double, false><<<grid, 256, 0, s>>>(d, wmax);
+        if (realw) kmax_kernel<double, true><<<grid, 256, 0, s>>>(d, kmax, wmax);
+        else kmax_kernel<double, false><<<grid, 256, 0, s>>>(d, kmax, wmax);
         tsplit_kernel<<<kSplitEntries / 256, 256, 0, s>>>(
             reinterpret_cast<C2<double>*>(reinterpret_cast<char*>(support) + tsplit_offset(d.nfreq)), d.n);
     }
