@@ -148,7 +148,9 @@ def test_bench_chunk_every_row(n, dtype, chunk, out_kind, kernel):
             ref = np.abs(ref_cwt[s]) ** 2
             assert np.max(np.abs(got - ref)) <= 2 * tol * np.max(ref), s
         # the same plan's complex output over the same chunks (same kernel family and block
-        # map): every row checked, and power == |cwt|^2 of it
+        # map): every row checked, and power == |cwt|^2 of it to 1e-6 of the signal's max (two
+        # instantiations whose fp32 FFT rounding may differ by a few ulps: 4.4e-7 measured on
+        # the bounds-checking debug build, whose code generation differs)
         out = torch.empty((S, F, n), dtype=cdt, device=dev)
         plan.execute(xd, out, out_kind='cwt')
         torch.cuda.synchronize()
@@ -158,7 +160,7 @@ def test_bench_chunk_every_row(n, dtype, chunk, out_kind, kernel):
             c2 = out[s0:s1].to(torch.complex128).abs() ** 2
             rel = float(((pw[s0:s1].to(torch.float64) - c2).abs().amax(dim=-1) /
                          c2.amax(dim=-1).clamp_min(1e-300)).max())
-            assert rel <= 4e-7, (s0, rel)
+            assert rel <= 1e-6, (s0, rel)
         del out, pw
     plan.close()
     torch.cuda.empty_cache()
