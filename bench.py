@@ -21,6 +21,7 @@ runs the same multi-rank flow on CPU without any kernel (tests/test_bench_cpu.py
 from __future__ import annotations
 
 import argparse
+import copy
 import hashlib
 import json
 import os
@@ -336,7 +337,8 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name, dtype
     el = max_over_ranks(torch, dist, el, dev if backend == 'nccl' else None)
     st = plan.stats()
     points = float(S) * F_all * n * args.steps * (1 if by_scales else world)
-    res = {'value': points / el, 'ms_per_step': el / args.steps * 1e3, 'dtype': 'f64' if f64 else 'f32',
+    res = {'value': points / el, 'ms_per_step': el / args.steps * 1e3, 'steps': args.steps, 'warmup': args.warmup,
+           'dtype': 'f64' if f64 else 'f32',
            'workload': text, 'kind': kind, 'epochs': epochs * (1 if by_scales else world), 'chans': chans,
            'n': n, 'freqs': freqs, 'F': F, 'F_all': F_all, 'out_kind': out_kind, 'chunk': C,
            'by_scales': by_scales, 'dtype_name': dtype, 'scale_slices': slices,
@@ -468,13 +470,18 @@ def roofline_of(args, cfg_name, st, S, F, n, C, out_kind, dtype, esz, el, L):
 # extra legs of the default line: key -> (config, compute dtype)
 LEGS = {'fp64': ('c4', 'float64'), 'c2': ('c2', 'float32'), 'c3': ('c3', 'float32'), 'c5': ('c5', 'float32'),
         'c5_fp64': ('c5', 'float64')}
+# at least this many timed steps / warmups for a leg whose step is short (C2: one 0.2-0.25 ms
+# launch; 3 steps time < 1 ms and vary +-10 % with the clock ramp), so each leg's timed region
+# runs >= ~10 ms; the headline line keeps exactly --steps / --warmup
+LEG_MIN_STEPS = {'c2': (40, 5)}
 
 
 def leg_fields(r, st, ex):
     """One extra leg's fields on the default line: its value, its workload, the dominant
     kernel's HBM roofline (+ the row pass's for the two-pass form), the VALU roofline and
     the end-to-end figure against the path's minimum traffic."""
-    d = {'value': r['value'], 'unit': 'points/s', 'ms_per_step': r['ms_per_step'], 'dtype': r['dtype'],
+    d = {'value': r['value'], 'unit': 'points/s', 'ms_per_step': r['ms_per_step'], 'steps': r['steps'],
+         'warmup': r['warmup'], 'dtype': r['dtype'],
          'workload': r['workload'], 'output': r['out_kind'], 'chunk_signals': r['chunk'], 'engine': st['engine'],
          'scaling': r['scaling'], 'parallelism': r['parallelism'], 'roofline': ex['roofline']}
     if r['scale_slices'] is not None:
@@ -583,7 +590,10 @@ def main(argv=None):
     leg_out = {}
     for leg in legs:
         cfg_name, dt = LEGS[leg]
-        r_, st_, ex_ = run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name,
+        largs = copy.copy(args)
+        ms, mw = LEG_MIN_STEPS.get(leg, (0, 0))
+        largs.steps, largs.warmup = max(args.steps, ms), max(args.warmup, mw)
+        r_, st_, ex_ = run_leg(largs, torch, dist, nw, L, world, rank, dev, backend, cfg_name,
                                dtype_override=dt, fp64_leg=(dt == 'float64'), overrides=(leg == 'fp64'))
         if rank == 0:
             leg_out[leg] = leg_fields(r_, st_, ex_)
