@@ -21,7 +21,7 @@
 //                per 1024-thread workgroup, C * 2e B contiguous per k1 read), epilogue y / |y|
 //                / |y|^2 stored to out[f][n2 + N2 n1] (256-B contiguous runs at N1 = 1024)
 //
-// fp64: E = 32 rows (16 for table rows), 16 elements per thread in the column pass, the
+// fp64: E = 32 rows (16 for table rows), 32 elements per thread in the column pass, the
 // column twiddles from two exact split tables and a per-thread recurrence, Morse rows in
 // the log domain (RowW<double>).
 //
@@ -52,7 +52,14 @@ constexpr int kRowTileG = 8;      // row groups per XCD tile
 // cols_kernel workgroups of 1024 threads: C = 32 columns at N1 = 1024, 256-B runs (C5 cols
 // 1.039 -> 0.978 ms per launch against 512 threads)
 // cols_kernel workgroup size (C * N1 / E)
+// fp64: 512 threads x 32 elements (N1 = 1024 in 2 passes, one exchange; 16 columns, 256-B runs
+// as before) against 1024 x 16 (3 passes, two exchanges): C5 fp64 cols 3.97-4.11 -> 3.90-3.91
+// ms per 32-scale launch (profiles/r05_c5f64_cols_e32_ab.txt; -DNW_COLS64_E16: the old form)
+#ifdef NW_COLS64_E16
 template <typename T> constexpr int kColThreads = 1024;
+#else
+template <typename T> constexpr int kColThreads = sizeof(T) == 8 ? 512 : 1024;
+#endif
 // bytes of B per launch pair (scales chunked to fit): 8 GiB = 64 scales of fp32 / 32 of fp64 at
 // C5.  Against 2 GiB (16 / 8 scales): C5 fp32 47.49 -> 46.15 ms per step, fp64 118.19 -> 113.15
 // (fewer, longer launches: the row pass's XCD tiles of 8 scales fill, fewer tails;
@@ -63,8 +70,12 @@ constexpr size_t kBBudget = size_t(8) << 30;
 template <typename T, int N2> constexpr int kRowE = N2 >= 8192 ? 32 : 16;
 // complex table rows (wavelet_bin loads) spill at fp64 E = 32: E = 16 there
 template <typename T, int N2> constexpr int kRowETab = sizeof(T) == 8 ? 16 : kRowE<T, N2>;
-// elements per thread in cols_kernel: 32 complex fp32 or 16 complex fp64 (64 VGPRs either way)
+// elements per thread in cols_kernel: 32 complex fp32 (64 VGPRs) or fp64 (128 VGPRs, 2 waves/SIMD)
+#ifdef NW_COLS64_E16
 template <typename T> constexpr int kColE = sizeof(T) == 4 ? 32 : 16;
+#else
+template <typename T> constexpr int kColE = 32;
+#endif
 // rows of at most 16384 on chip, fp64 too (N2 = 8192 with N1 = 2048, 8-column blocks and
 // 128-B runs: C5 fp64 150.0 ms/step; 16384, 16 columns, 256-B runs: 129.9)
 template <typename T> constexpr int kMaxN2 = 16384;
@@ -690,7 +701,11 @@ constexpr int kSplitLo = 4096;
 constexpr int kSplitEntries = 2 * kSplitLo;   // n <= 2^24: m >> 12 < 4096
 
 template <typename T, int N1, int N2, int OUT>
+#ifdef NW_COLS64_E16
 __global__ __launch_bounds__(kColThreads<T>, sizeof(T) == 8 ? 2 : 4) void cols_kernel(
+#else
+__global__ __launch_bounds__(kColThreads<T>, sizeof(T) == 8 ? 1 : 4) void cols_kernel(
+#endif
     int f0, int nf, const C2<T>* __restrict__ B, void* __restrict__ out, const C2<T>* __restrict__ tw1,
     const C2<T>* __restrict__ tsplit) {
     using CL = Cols<T, N1>;

@@ -18,7 +18,7 @@ SWITCHES = {
                      'NW_PAIR_PAD16=0', 'NW_TAIL_EXACT'],
     'nw_large.hip': ['NW_ABL_ROWS_NOW', 'NW_B_PLAIN', 'NW_ABL_COLS_NOFFT', 'NW_ABL_COLS_NOSTORE',
                      'NW_ABL_COLS_NOTW', 'NW_ABL_COLS_STREAM', 'NW_ABL_ROWS_STREAM', 'NW_ABL_NOSTORE', 'NW_ABL_NOTWIDDLE', 'NW_ABL_NOEXCH',
-                     'NW_ROWS_NO_REC', 'NW_TAIL_EXACT'],
+                     'NW_ROWS_NO_REC', 'NW_TAIL_EXACT', 'NW_COLS64_E16'],
 }
 
 
