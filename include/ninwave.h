@@ -190,6 +190,15 @@ int nw_plan_wavelet_shape(nw_plan* plan, int64_t* len_full, int64_t* row_len);
  * table kinds) -- the reference's self.fft_wavelets. */
 int nw_plan_wavelet_rows(nw_plan* plan, void* out_host);
 
+/* Diagnostic: the W-row support the two-pass engine (2^15 <= n <= 2^24) prunes its row pass
+ * to -- kmax_out[nfreq] = the last bin k whose |W_f[k]| exceeds the tail threshold (2^-72 fp64,
+ * 2^-56 fp32, of the row's max |W|; -1 for an all-zero row) of every scale of the plan.  method
+ * 0: as the engine builds it (no full scan for Morse / Morlet / Shannon rows), 1: by scanning every bin
+ * (the reference the tests compare method 0 with).  No reference counterpart: the reference
+ * multiplies every bin (base.py:404-406); the cut bins together move y by < n * 2^-72 (fp64)
+ * of the signal's scale.  NW_E_STATE for plans on another engine. */
+int nw_plan_row_support(nw_plan* plan, int method, int32_t* kmax_out);
+
 /* Run the CWT of nsig signals x[nsig][n] (plan dtype) into out[nsig][nfreq][n]
  * (complex for NW_OUT_CWT, real otherwise), or (F, N) for the reduction kinds
  * NW_OUT_POWER_MEAN .. NW_OUT_PHASE_SUM.  mem = NW_MEM_HOST: synchronous;

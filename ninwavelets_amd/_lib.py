@@ -82,6 +82,7 @@ SIGNATURES = [
                                            ctypes.POINTER(ctypes.c_int64)]),
     ('nw_plan_wavelet_shape', ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
     ('nw_plan_wavelet_rows', ctypes.c_int, [_P, _P]),
+    ('nw_plan_row_support', ctypes.c_int, [_P, ctypes.c_int, _P]),
     ('nw_execute', ctypes.c_int, [_P, _P, _I64, _P, ctypes.c_int, ctypes.c_int]),
     ('nw_execute_multi', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),
     ('nw_execute_multi_scales', ctypes.c_int, [ctypes.POINTER(_P), ctypes.c_int, _P, _I64, _P, ctypes.c_int]),

@@ -260,7 +260,10 @@ int take_event(nw_plan* p, hipEvent_t* ev) {
         p->event_pool.pop_back();
         return NW_OK;
     }
-    NW_HIP(hipEventCreate(ev));
+    // timing only (resolve_timing synchronises the stream before reading them): no system-scope
+    // fence at record, whose L2 writeback + invalidate between a step's two launches cost C2
+    // (one 0.23 ms launch per step) 0.04 ms per step and showed up in the stage times
+    NW_HIP(hipEventCreateWithFlags(ev, hipEventDisableSystemFence));
     return NW_OK;
 }
 
@@ -314,6 +317,16 @@ int resolve_timing(nw_plan* p) {
     }
     p->pending.clear();
     return NW_OK;
+}
+
+// execute-time geometry: pad_to the cached rows to n, mask X (base.py:396-401)
+void set_exec_geometry(nw_plan* p) {
+    nw::WDesc& d = p->desc;
+    d.n = p->n;
+    d.nh = p->nh;
+    d.scale = 1.0 / (double)p->n;
+    d.off = d.len_full < p->n ? (p->n - d.len_full) / 2 : 0;
+    d.xlim = (p->flags & NW_INTERPOLATE) ? p->n / 2 : p->n;   // int(n / 2) (base.py:120)
 }
 
 rocfft_precision prec(const nw_plan* p) {
@@ -1235,6 +1248,27 @@ int nw_plan_wavelet_rows(nw_plan* p, void* out_host) {
     return NW_OK;
 }
 
+int nw_plan_row_support(nw_plan* p, int method, int32_t* kmax_out) {
+    if (!p || !kmax_out) return fail(NW_E_INVALID, "nw_plan_row_support: null argument");
+    if (!p->has_wavelet) return fail(NW_E_STATE, "nw_plan_row_support: no wavelet attached");
+    if (!p->large || p->engine == NW_ENGINE_ROCFFT)
+        return fail(NW_E_STATE, "nw_plan_row_support: the plan does not run the two-pass engine");
+    if (method != 0 && method != 1) return fail(NW_E_INVALID, "nw_plan_row_support: bad method");
+    DeviceGuard guard(p->device);
+    set_exec_geometry(p);
+    // into a scratch buffer (the plan's own support stays as built: under a repeated-rows view
+    // it holds the distinct rows only)
+    void* tmp = nullptr;
+    NW_HIP(hipMalloc(&tmp, nw::large_support_bytes(p->nfreq)));
+    hipError_t e = nw::large_row_support(p->desc, p->dtype, tmp, method == 1, p->stream);
+    const void* src = tmp;
+    if (e == hipSuccess) e = hipMemcpyAsync(kmax_out, src, (size_t)p->nfreq * sizeof(int32_t), hipMemcpyDeviceToHost, p->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(p->stream);
+    if (tmp) (void)hipFree(tmp);
+    if (e != hipSuccess) return fail(NW_E_HIP, std::string("nw_plan_row_support: ") + hipGetErrorString(e));
+    return NW_OK;
+}
+
 int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind, int mem) {
     if (!p || (!x && nsig > 0) || (!out && nsig > 0)) return fail(NW_E_INVALID, "nw_execute: null argument");
     if (!p->has_wavelet) return fail(NW_E_STATE, "nw_execute: nw_plan_set_wavelet first");
@@ -1244,13 +1278,7 @@ int nw_execute(nw_plan* p, const void* x, int64_t nsig, void* out, int out_kind,
     if (is_reduction(out_kind) && !out) return fail(NW_E_INVALID, "nw_execute: null out");
     if (nsig == 0 && !is_reduction(out_kind)) return NW_OK;
     DeviceGuard guard(p->device);
-    // execute-time geometry: pad_to the cached rows to n, mask X (base.py:396-401)
-    nw::WDesc& d = p->desc;
-    d.n = p->n;
-    d.nh = p->nh;
-    d.scale = 1.0 / (double)p->n;
-    d.off = d.len_full < p->n ? (p->n - d.len_full) / 2 : 0;
-    d.xlim = (p->flags & NW_INTERPOLATE) ? p->n / 2 : p->n;   // int(n / 2) (base.py:120)
+    set_exec_geometry(p);
     if (p->chirp && p->chirp_tentative && !p->wtab_valid) {   // settle the engine before any buffer choice
         if (p->dedup) {
             UniqueRows u(p);

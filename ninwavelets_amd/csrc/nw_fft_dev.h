@@ -479,6 +479,10 @@ template <typename T, int N, int E> struct Tab1 {
     // (nw_fused.hip: C4 shape fp64 8.19-8.21 -> 7.96 ms per launch, 0.525 -> 0.541 of HBM peak;
     // the C5 fp64 row pass +-0 with it and its step 3 % slower, so nw_large.hip keeps the bases;
     // profiles/r05_f64_tab1_ab.txt)
+    // (A per-file choice without an ODR question: this header's templates live in an unnamed
+    // namespace, so every translation unit instantiates its own Tab1 -- internal linkage, as
+    // `static` -- and nw_fused.hip's Tab1<double, 16384, 32> is not nw_large.hip's; the
+    // device code is compiled per file, without -fgpu-rdc, too.)
 #ifdef NW_TAB1_F64_16384
     static constexpr bool BIG = sizeof(S) == 8 && N == 16384 && E == 32;
 #else

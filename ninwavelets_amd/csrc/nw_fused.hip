@@ -88,6 +88,26 @@ constexpr bool kPairXD = true;
 template <typename T, int N, int E> constexpr bool kNz24Of = kNz24 && E > 16;
 // NZ = 12 and 20 between them (fp32 only: fp64 n = 16384 |y| spills 20 B with them)
 template <typename T, int N, int E> constexpr bool kNzFineOf = kNz24Of<T, N, E> && sizeof(T) == 4;
+// ... and for the fp64 cwt output (-DNW_F64_FINE: diagnostic A/B; its |y| spills with them)
+#ifdef NW_F64_FINE
+template <typename T, int N, int E, int OUT> constexpr bool kNzFineOut = kNzFineOf<T, N, E> ||
+    (kNz24Of<T, N, E> && OUT == NW_OUT_CWT);
+#else
+template <typename T, int N, int E, int OUT> constexpr bool kNzFineOut = kNzFineOf<T, N, E>;
+#endif
+// The pass-0 variant (elements read and multiplied per thread) that runs a row of support nz:
+// the smallest instantiated NZ >= nz.  The X LDS-DMA copies what THAT variant reads (a row
+// of support 12 on a kernel without the NZ = 12 variant runs NZ = 16, which reads 16 elements)
+template <typename T, int N, int E, int OUT>
+__device__ __forceinline__ int pass0_variant(int nz) {
+    if (nz <= 4) return 4;
+    if (nz <= 8) return 8;
+    if (kNzFineOut<T, N, E, OUT> && nz <= 12) return 12;
+    if (E > 16 && nz <= 16) return 16;
+    if (kNzFineOut<T, N, E, OUT> && nz <= 20) return 20;
+    if (kNz24Of<T, N, E> && nz <= 24) return 24;
+    return E;
+}
 // signals per block: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (2 and 16 slower or equal).
 // fp64 (one block per CU) takes 4: an XCD round of 8 scales x 4 groups then reads W (8 x 128
 // KiB) + X (16 x 128 KiB) = 3 MiB, inside the XCD's 4 MiB L2 (8 signals: 5 MiB, re-read from
@@ -95,12 +115,28 @@ template <typename T, int N, int E> constexpr bool kNzFineOf = kNz24Of<T, N, E> 
 // 9.55 / 9.40, 16: 9.71; two boxes, tools/ab.sh)
 constexpr int kGroup = 8;
 static_assert(kGroup == kPsumGroup, "fused partial rows are counted by fused_psum_groups");
-constexpr int kGroup64 = 4;
+// (-DNW_GROUP64 / NW_TILE64_F / NW_TILE64_G: diagnostic A/B of the fp64 block and tile shape)
+#ifndef NW_GROUP64
+#define NW_GROUP64 4
+#endif
+constexpr int kGroup64 = NW_GROUP64;
 // XCD tile: kTileF scales x kTileG signal groups per XCD round (fp64 tiles 16 x 2, 4 x 8,
 // 32 x 1, 2 x 16 measured -2.4 / -0.2 / -4.8 / -3.5 % against 8 x 4)
 constexpr int kTileF = 8, kTileG = 4;
-template <typename T> constexpr int kTileFT = kTileF;
-template <typename T> constexpr int kTileGT = kTileG;
+#ifndef NW_TILE64_F
+#define NW_TILE64_F kTileF
+#endif
+#ifndef NW_TILE64_G
+#define NW_TILE64_G kTileG
+#endif
+template <typename T> constexpr int kTileFT = sizeof(T) == 8 ? NW_TILE64_F : kTileF;
+template <typename T> constexpr int kTileGT = sizeof(T) == 8 ? NW_TILE64_G : kTileG;
+// ... and at most as many groups as a launch has (in units of 8 XCD slots): C2 (64 signals =
+// 8 groups) with 4-group tiles padded its grid to 4x its real blocks
+__host__ __device__ constexpr int tile_g_of(int64_t nsg, int tg_max) {
+    const int64_t per = (nsg + 7) / 8;
+    return per < tg_max ? (int)(per < 1 ? 1 : per) : tg_max;
+}
 // Occupancy: 4 waves/SIMD (128 VGPRs) for fp32 -- the half image is <= 74 KiB, so two
 // 512-thread blocks share a CU at n = 16384 (more at smaller n) and one block's barriers,
 // memory waits and store bursts overlap another's arithmetic -- and 2 for fp64 (twice the
@@ -126,7 +162,7 @@ template <typename T, int N, int E, int OUT, bool REALW, int WSH = 0>
 __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WDesc d, const cplx<T>* __restrict__ X,
                                                             const void* __restrict__ wtab, void* __restrict__ out,
                                                             const C2<T>* __restrict__ tw, int64_t nsig, int group,
-                                                            int nsg_pad, const int* __restrict__ wnz) {
+                                                            int nsg_pad, const int* __restrict__ wnz, int tg) {
     using G = Geometry<N, E>;
     using WT = typename WLoad<T, REALW>::type;
     constexpr bool XD = kXDMA<T, E, REALW>;
@@ -148,12 +184,12 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     const int b = blockIdx.x;
     const int xcd = b & 7;
     const int local = b >> 3;
-    constexpr int TF = kTileFT<T>, TG = kTileGT<T>;
-    const int pos = local % (TF * TG);
-    const int round = local / (TF * TG);
+    constexpr int TF = kTileFT<T>;
+    const int pos = local % (TF * tg);
+    const int round = local / (TF * tg);
     const int nfr = (d.nfreq + TF - 1) / TF;
     const int fi = (round % nfr) * TF + pos % TF;
-    const int sg = ((round / nfr) * TG + pos / TF) * 8 + xcd;
+    const int sg = ((round / nfr) * tg + pos / TF) * 8 + xcd;
     if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
     const int64_t s_begin = (int64_t)sg * group;
     const int64_t s_end = min(nsig, s_begin + group);
@@ -207,8 +243,7 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     C2<T> nyq{T(0), T(0)};
     if constexpr (XD) {
         nyq = reinterpret_cast<const C2<T>*>(X + s_begin * d.nh)[N / 2];
-        const int nz0 = max(1, wnz[fi] >> WSH);
-        const int nzv0 = nz0 < kPruneMin ? kPruneMin : nz0;
+        const int nzv0 = pass0_variant<T, N, E, OUT>(max(1, wnz[fi] >> WSH));
         dma_x<T, N, G::T>(reinterpret_cast<const C2<T>*>(X + s_begin * d.nh),
                           lds, t, nzv0 <= E / 2 ? dma_rounds_for<T>(nzv0) : 1 << 30);
     }
@@ -218,8 +253,10 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
     const int nz = max(1, wnz[fi] >> WSH);
     NW_DCHECK(fi < d.nfreq && s_end <= nsig && d.n == N && nz <= E);
     // LDS-DMA only the X bins the pruned pass 0 reads: variant NZ (>= 4) reads bins < NZ*T,
-    // i.e. NZ/2 rounds of 2*T bins, when it reads no mirrored bin (NZ <= E/2)
-    const int nzv = nz < kPruneMin ? kPruneMin : nz;
+    // i.e. NZ/2 rounds of 2*T bins (fp32; NZ rounds of T bins in fp64), when it reads no
+    // mirrored bin (NZ <= E/2)
+    const int nzv = pass0_variant<T, N, E, OUT>(nz);
+    static_assert(kPruneMin == 4, "the smallest pass-0 variant");
     const int dma_rounds = nzv <= E / 2 ? dma_rounds_for<T>(nzv) : 1 << 30;
     // power partial sums (kOutPSum): sum over the block's signals of |y|^2 per output point
     // (kOutPhSum: the sums of y / |y|, two fp64 values per point)
@@ -270,12 +307,12 @@ __global__ __launch_bounds__(N / E, (kWpsOf<T, E, OUT>)) void nw_fused_kernel(WD
                 v[r] = r < NZ ? WLoad<T, REALW>::apply(w_at(r), x[r]) : C2<T>{T(0), T(0)};
             idft_br<T, E, NZ>(v);
         };
-        if (nz <= 4) pass0.template operator()<4>();
-        else if (nz <= 8) pass0.template operator()<8>();
-        else if (kNzFineOf<T, N, E> && nz <= 12) pass0.template operator()<(E > 16 ? 12 : E)>();
-        else if (E > 16 && nz <= 16) pass0.template operator()<(E > 16 ? 16 : E)>();
-        else if (kNzFineOf<T, N, E> && nz <= 20) pass0.template operator()<(E > 16 ? 20 : E)>();
-        else if (kNz24Of<T, N, E> && nz <= 24) pass0.template operator()<(E > 16 ? 24 : E)>();
+        if (nzv == 4) pass0.template operator()<4>();
+        else if (nzv == 8) pass0.template operator()<8>();
+        else if (kNzFineOut<T, N, E, OUT> && nzv == 12) pass0.template operator()<(E > 16 ? 12 : E)>();
+        else if (E > 16 && nzv == 16) pass0.template operator()<(E > 16 ? 16 : E)>();
+        else if (kNzFineOut<T, N, E, OUT> && nzv == 20) pass0.template operator()<(E > 16 ? 20 : E)>();
+        else if (kNz24Of<T, N, E> && nzv == 24) pass0.template operator()<(E > 16 ? 24 : E)>();
         else pass0.template operator()<E>();
         if constexpr (XD) {
             if (s + 1 < s_end) nyq = sload_c2(reinterpret_cast<const C2<T>*>(X + (s + 1) * d.nh) + N / 2);
@@ -324,7 +361,8 @@ template <int N, int E, int OUT>
 __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_kernel(WDesc d, const cplx<float>* __restrict__ X,
                                                                   const void* __restrict__ wtab, void* __restrict__ out,
                                                                   const C2<float>* __restrict__ tw, int64_t nsig,
-                                                                  int group, int nsg_pad, const int* __restrict__ wnz) {
+                                                                  int group, int nsg_pad, const int* __restrict__ wnz,
+                                                                  int tg) {
     using G = Geometry<N, E>;
     static_assert(E <= 16, "pair mode holds 2 x E complex values per lane");
     extern __shared__ __align__(16) unsigned char smem[];
@@ -334,11 +372,11 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
     const int b = blockIdx.x;
     const int xcd = b & 7;
     const int local = b >> 3;
-    const int pos = local % (kTileF * kTileG);
-    const int round = local / (kTileF * kTileG);
+    const int pos = local % (kTileF * tg);
+    const int round = local / (kTileF * tg);
     const int nfr = (d.nfreq + kTileF - 1) / kTileF;
     const int fi = (round % nfr) * kTileF + pos % kTileF;
-    const int sg = ((round / nfr) * kTileG + pos / kTileF) * 8 + xcd;
+    const int sg = ((round / nfr) * tg + pos / kTileF) * 8 + xcd;
     if (fi >= d.nfreq || sg >= nsg_pad || (int64_t)sg * group >= nsig) return;
     const int64_t s_begin = (int64_t)sg * group;
     // the block's signal count, pinned in an SGPR: as an int64 min it sat in a VGPR pair that
@@ -639,7 +677,8 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     if (e != hipSuccess) return e;
     const int grp = sizeof(T) == 8 ? kGroup64 : kGroup;
     const int64_t nsg = (nsig + grp - 1) / grp;
-    constexpr int TF = kTileFT<T>, TG = kTileGT<T>;
+    constexpr int TF = kTileFT<T>;
+    const int TG = tile_g_of(nsg, kTileGT<T>);
     const int64_t nsg_pad = (nsg + 8 * TG - 1) / (8 * TG) * (8 * TG);
     const int64_t nfr = (d.nfreq + TF - 1) / TF;
     const int64_t blocks = nsg_pad * nfr * TF;
@@ -653,19 +692,19 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
         const C2<float>* twf = reinterpret_cast<const C2<float>*>(tw);
         const cplx<float>* Xf = reinterpret_cast<const cplx<float>*>(X);
         if (out_kind == NW_OUT_CWT)
-            nw_fused_pair_kernel<N, E, NW_OUT_CWT><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz);
+            nw_fused_pair_kernel<N, E, NW_OUT_CWT><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
         else if (out_kind == NW_OUT_POWER)
-            nw_fused_pair_kernel<N, E, NW_OUT_POWER><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz);
+            nw_fused_pair_kernel<N, E, NW_OUT_POWER><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
         else
-            nw_fused_pair_kernel<N, E, NW_OUT_ABS><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz);
+            nw_fused_pair_kernel<N, E, NW_OUT_ABS><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
         return hipGetLastError();
     }
     if (out_kind == NW_OUT_CWT)
-        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz);
+        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
     else if (out_kind == NW_OUT_POWER)
-        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz);
+        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
     else
-        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz);
+        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
     return hipGetLastError();
 }
 
@@ -680,7 +719,8 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
                             hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     const int64_t nsg = (nsig + kGroup - 1) / kGroup;
-    constexpr int TF = kTileFT<T>, TG = kTileGT<T>;
+    constexpr int TF = kTileFT<T>;
+    const int TG = tile_g_of(nsg, kTileGT<T>);
     const int64_t nsg_pad = (nsg + 8 * TG - 1) / (8 * TG) * (8 * TG);
     const int64_t nfr = (d.nfreq + TF - 1) / TF;
     const int64_t blocks = nsg_pad * nfr * TF;
@@ -695,12 +735,12 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
         if (e != hipSuccess) return e;
         nw_fused_pair_kernel<N, E, kOutPSum><<<blocks, threads, lp, s>>>(
             d, reinterpret_cast<const cplx<float>*>(X), wtab, partials, reinterpret_cast<const C2<float>*>(tw), nsig,
-            kGroup, (int)nsg_pad, wnz);
+            kGroup, (int)nsg_pad, wnz, TG);
         return hipGetLastError();
     }
     nw_fused_kernel<T, N, E, OUT, true, WSH><<<blocks, threads, lds, s>>>(
         d, reinterpret_cast<const cplx<T>*>(X), wtab, partials, reinterpret_cast<const C2<T>*>(tw), nsig, kGroup,
-        (int)nsg_pad, wnz);
+        (int)nsg_pad, wnz, TG);
     return hipGetLastError();
 }
 

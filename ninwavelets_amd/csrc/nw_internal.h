@@ -267,6 +267,9 @@ size_t     large_scratch_bytes(int64_t n, int nfreq, int dtype);
 size_t     large_support_bytes(int nfreq);
 int64_t    large_fchunk(int64_t n, int nfreq, int dtype);
 hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStream_t s);
+// kmax[] / wmax[] of the rows into support (its first nfreq ints are kmax): the analytic kinds
+// without a full scan (support_fast_kernel), the others -- or scan = true -- by scanning every bin
+hipError_t large_row_support(const WDesc& d, int dtype, void* support, bool scan, hipStream_t s);
 hipError_t large_transpose(const WDesc& d, int dtype, const void* X, void* scratch, hipStream_t s);
 hipError_t large_rows(const WDesc& d, int dtype, int f0, int nf, const void* support, void* scratch, hipStream_t s);
 hipError_t large_cols(const WDesc& d, int dtype, int out_kind, int f0, int nf, const void* support,

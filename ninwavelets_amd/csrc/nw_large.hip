@@ -136,6 +136,157 @@ __global__ __launch_bounds__(256) void kmax_kernel(WDesc d, int* __restrict__ km
     if ((threadIdx.x & 63) == 0 && m >= 0) atomicMax(&kmax[fi], m);
 }
 
+// ---- The same wmax[f] and kmax[f] for the analytic kinds without a full scan.  A Morse,
+// Morlet (sigma > 0) or Shannon row is unimodal in k: |psi| rises to its peak (Morse nu = f,
+// Morlet x = nu/f p(f) ~ sigma, Shannon k = 0) and falls after it (the computed value c(k) is
+// the true g(x_k) times (1 + e_k), |e_k| <= eps, with x_k monotone in k).  One 256-thread block
+// per row, O(window + F log n) evaluations of the scan's own wmag instead of 2 n:
+//  1. max: scan a window around the analytic peak, widened 4x until both window edges lie
+//     at the row's ends or below M (1 - kMu); then no bin outside exceeds the window's max M
+//     (if g rose past an edge, that edge would be within 2 eps of M; if it fell, every bin
+//     beyond is below the edge's value times (1 + 3 eps)), so M is the full scan's max.
+//  2. kmax: a 256-ary bisection on [argmax, end) for a bin J with c(J) <= L = thr (1 - kMu);
+//     every bin past J is then <= L (1 + 3 eps) < thr, so the last bin above thr lies in
+//     [argmax, J): a backward scan from J finds it -- the full scan's kmax.
+// kMu >> 3 eps: fp64 evaluations are within ~1e-12 relative wherever they matter, fp32's
+// log2-domain Morse within ~3e-5 (v_log / v_exp on exponents of magnitude <= 200).
+// Plans whose rows may hold non-finite bins (morse_ovf), tables, sigma <= 0, b <= 0 and the
+// exact support (kTailRel = 0) keep wmax_kernel / kmax_kernel; a row that still meets a
+// non-finite value here is scanned whole by its block (the scan kernels' rules).
+template <typename T> constexpr double kMu = sizeof(T) == 8 ? 0x1p-30 : 0x1p-10;
+constexpr int kFastThreads = 256, kFastBins = 16;   // bins per thread per scan round
+
+bool support_fast_ok(const WDesc& d, int dtype) {
+    if ((dtype == NW_F32 ? kTailRel<float> : kTailRel<double>) == 0.0) return false;
+    if (d.kind == NW_MORSE) return !d.morse_ovf && d.b > 0.0 && d.r > 0.0;
+    if (d.kind == NW_MORLET) return d.sigma > 0.0;
+    return d.kind == NW_SHANNON;
+}
+
+// block reductions over kFastThreads threads (4 waves): max with its (smallest) bin, min bin
+__device__ __forceinline__ void blk_max_arg(double& v, int64_t& k, double* sv, int64_t* sk) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const double v2 = __shfl_xor(v, o, 64);
+        const int64_t k2 = __shfl_xor(k, o, 64);
+        if (v2 > v || (v2 == v && k2 < k)) { v = v2; k = k2; }
+    }
+    const int w = threadIdx.x >> 6;
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) { sv[w] = v; sk[w] = k; }
+    __syncthreads();
+    v = sv[0]; k = sk[0];
+    for (int i = 1; i < kFastThreads / 64; ++i)
+        if (sv[i] > v || (sv[i] == v && sk[i] < k)) { v = sv[i]; k = sk[i]; }
+}
+__device__ __forceinline__ int64_t blk_min_i64(int64_t k, int64_t* sk) {
+    for (int o = 32; o > 0; o >>= 1) k = min(k, (int64_t)__shfl_xor(k, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sk[threadIdx.x >> 6] = k;
+    __syncthreads();
+    for (int i = 0; i < kFastThreads / 64; ++i) k = min(k, sk[i]);
+    return k;
+}
+__device__ __forceinline__ int64_t blk_max_i64(int64_t k, int64_t* sk) {
+    for (int o = 32; o > 0; o >>= 1) k = max(k, (int64_t)__shfl_xor(k, o, 64));
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sk[threadIdx.x >> 6] = k;
+    __syncthreads();
+    for (int i = 0; i < kFastThreads / 64; ++i) k = max(k, sk[i]);
+    return k;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kFastThreads) void support_fast_kernel(WDesc d, int* __restrict__ kmax,
+                                                                    unsigned long long* __restrict__ wmax) {
+    __shared__ double sv[kFastThreads / 64];
+    __shared__ int64_t sk[kFastThreads / 64];
+    const int fi = blockIdx.x;
+    const int t = threadIdx.x;
+    const int64_t lim = d.xlim < d.n ? d.xlim : d.n;
+    const int64_t lo = d.off > 0 ? d.off : 0;
+    const int64_t hi = min(lim, d.off + d.len_valid);   // W = 0 outside [lo, hi)
+    if (hi <= lo) return;                                // kmax -1, wmax 0 (memset)
+    auto mag = [&](int64_t k) { return wmag<T, true>(d, fi, k); };
+    // the analytic peak's row bin j* (x = 1 for Morse, x = sigma for Morlet, 0 for Shannon)
+    const double f = d.freq[fi];
+    double js = 0.0;
+    if (d.kind == NW_MORSE) js = f / d.delta;
+    else if (d.kind == NW_MORLET) js = d.sigma * f / (d.peak[fi] * d.delta);
+    const double kd = (double)d.off + (js == js ? js : 0.0);
+    const int64_t kp = kd <= (double)lo ? lo : kd >= (double)(hi - 1) ? hi - 1 : (int64_t)kd;
+    bool bad = false;
+    // 1. the row max over a widening window around the peak
+    double M = 0.0;
+    int64_t m = lo;
+    for (int64_t w = kFastThreads * kFastBins / 2;; w *= 4) {
+        const int64_t a = max(lo, kp - w), b = min(hi - 1, kp + w);
+        double v = -1.0;
+        int64_t kv = b;
+        for (int64_t k = a + t; k <= b; k += kFastThreads) {
+            const double c = mag(k);
+            if (!(c <= 1.7976931348623157e308)) bad = true;
+            else if (c > v) { v = c; kv = k; }
+        }
+        if (__syncthreads_or(bad)) break;
+        blk_max_arg(v, kv, sv, sk);
+        M = v;
+        m = kv;
+        const double edge = M * (1.0 - kMu<T>);
+        if ((a == lo || mag(a) <= edge) && (b == hi - 1 || mag(b) <= edge)) break;
+    }
+    if (bad) {
+        // the scan kernels' rules over the whole row: the max of the finite bins, then the last
+        // bin above the threshold with non-finite bins in the support
+        double v = 0.0;
+        int64_t kv = lo;
+        for (int64_t k = lo + t; k < hi; k += kFastThreads) v = fmax(v, tail_max_term(mag(k)));
+        blk_max_arg(v, kv, sv, sk);
+        const double thr = kTailRel<T> * v;
+        int64_t found = -1;
+        for (int64_t k = lo + t; k < hi; k += kFastThreads)
+            if (tail_in_support(mag(k), thr)) found = k;
+        found = blk_max_i64(found, sk);
+        if (t == 0) {
+            wmax[fi] = (unsigned long long)__double_as_longlong(v);
+            kmax[fi] = (int)found;
+        }
+        return;
+    }
+    if (M <= 0.0) return;                               // an all-zero row: kmax -1, wmax 0
+    const double thr = kTailRel<T> * M;
+    const double L = thr * (1.0 - kMu<T>);
+    // 2. a bin J >= m with c(J) <= L: 256-ary bisection on [m, hi); J = hi when none
+    int64_t l = m, r = hi;                              // c(l) > L; c(r) <= L or r = hi
+    if (mag(hi - 1) <= L) {
+        r = hi - 1;
+        while (r - l > 1) {
+            const int64_t span = r - l;
+            // sample points l + span * (t + 1) / 257 (distinct when span > 256)
+            const int64_t p = l + (span > kFastThreads ? span * (t + 1) / (kFastThreads + 1) : t + 1);
+            const bool below = p < r && mag(p) <= L;
+            const int64_t first = blk_min_i64(below ? p : r, sk);   // first sampled bin <= L
+            // the sample before it (or l) stays above L
+            const int64_t prev = blk_max_i64(p < first ? p : l, sk);
+            l = prev;
+            r = first;
+        }
+    }
+    // 3. the last bin above thr in [m, r): backward scan from r - 1 (c(m) = M > thr ends it)
+    int64_t km = -1;
+    for (int64_t top = r - 1; km < 0 && top >= m; top -= kFastThreads * kFastBins) {
+        int64_t found = -1;
+        for (int i = 0; i < kFastBins; ++i) {
+            const int64_t k = top - (int64_t)i * kFastThreads - t;
+            if (k >= m && k > found && tail_in_support(mag(k), thr)) found = k;
+        }
+        km = blk_max_i64(found, sk);
+    }
+    if (t == 0) {
+        wmax[fi] = (unsigned long long)__double_as_longlong(M);
+        kmax[fi] = (int)km;
+    }
+}
+
 // ---- W_f[k] of one scale in fp32 for a compile-time kind: psi_f32 (nw_internal.h) with
 // the same operations in the same order, times 1/n, as wavelet_bin<float> -- so a row
 // here equals the nw_fused W table bit for bit -- but on 32-bit bin indices (n <= 2^24)
@@ -246,15 +397,17 @@ struct ExpK {
         }
     }
 };
-// FINITE: y is known finite and <= 21.4 (the b = 17.5 rows' valid bins): no NaN pass-through,
-// and the lower bound by one v_max_f64 against a plain constant
+// FINITE: y is finite (the b = 17.5 rows): no NaN pass-through, and both bounds by plain
+// constants.  Valid bins have y <= 21.4; the branch-free kMorseFast35 / kMorseRec evaluators also
+// evaluate the bins before a row's start (j < 0, x < 0: y = (b/r)(1 - x^3) up to ~1e9), whose
+// values the final select drops -- the upper clamp keeps rint(y log2 e) inside int there too
 template <bool FINITE = false>
 __device__ __forceinline__ double exp_rows(double y, const ExpK& K) {
     // k fits an int: y is bounded below here (NaN -> the bound, fixed at the end); above by the
     // fast Morse form's domain, y = (b/r)(1 - x^3) <= b/3 < 21.4 (a select, not fmax: fmax
     // canonicalises its opaque SGPR operand with two extra v_max per call)
     double yc;
-    if constexpr (FINITE) yc = fmax(y, -1100.0);
+    if constexpr (FINITE) yc = fmin(fmax(y, -1100.0), 1100.0);
     else yc = y > K.lo ? y : K.lo;
     const double k = __builtin_rint(yc * K.log2e);
     double rr = fma(-k, K.ln2hi, yc);
@@ -1031,13 +1184,21 @@ size_t large_scratch_bytes(int64_t n, int nfreq, int dtype) {
 
 size_t large_support_bytes(int nfreq) { return tsplit_offset(nfreq) + kSplitEntries * sizeof(C2<double>); }
 
-hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStream_t s) {
+// kmax[] and wmax[] of every row into `support`: the analytic kinds by support_fast_kernel,
+// the others (or scan = true: the full-scan reference the tests compare it with) by
+// wmax_kernel + kmax_kernel over every bin
+hipError_t large_row_support(const WDesc& d, int dtype, void* support, bool scan, hipStream_t s) {
     int* kmax = reinterpret_cast<int*>(support);
     auto* wmax = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(support) + wmax_offset(d.nfreq));
     hipError_t e = hipMemsetAsync(kmax, 0xFF, (size_t)d.nfreq * sizeof(int), s);   // -1
     if (e != hipSuccess) return e;
     e = hipMemsetAsync(wmax, 0, (size_t)d.nfreq * sizeof(uint64_t), s);            // +0.0
     if (e != hipSuccess) return e;
+    if (!scan && support_fast_ok(d, dtype)) {
+        if (dtype == NW_F32) support_fast_kernel<float><<<d.nfreq, kFastThreads, 0, s>>>(d, kmax, wmax);
+        else support_fast_kernel<double><<<d.nfreq, kFastThreads, 0, s>>>(d, kmax, wmax);
+        return hipGetLastError();
+    }
     const int64_t per_block = 256 * kSupBins;
     dim3 grid((unsigned)((d.n + per_block - 1) / per_block), (unsigned)d.nfreq);
     const bool realw = d.kind != NW_TABLE;
@@ -1051,6 +1212,19 @@ hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStre
         else wmax_kernel<double, false><<<grid, 256, 0, s>>>(d, wmax);
         if (realw) kmax_kernel<double, true><<<grid, 256, 0, s>>>(d, kmax, wmax);
         else kmax_kernel<double, false><<<grid, 256, 0, s>>>(d, kmax, wmax);
+    }
+    return hipGetLastError();
+}
+
+hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStream_t s) {
+    // NW_SUPPORT_SCAN=1: every row by the full scan (diagnostic A/B)
+    static const bool force_scan = [] {
+        const char* v = std::getenv("NW_SUPPORT_SCAN");
+        return v && v[0] == '1';
+    }();
+    hipError_t e = large_row_support(d, dtype, support, force_scan, s);
+    if (e != hipSuccess) return e;
+    if (dtype == NW_F64) {
         tsplit_kernel<<<kSplitEntries / 256, 256, 0, s>>>(
             reinterpret_cast<C2<double>*>(reinterpret_cast<char*>(support) + tsplit_offset(d.nfreq)), d.n);
     }

@@ -87,12 +87,31 @@ class HostPool:
 
     @staticmethod
     def _nw_advise(arr):
-        L.check(L.lib().nw_host_advise(ctypes.c_void_p(arr.ctypes.data), int(arr.nbytes), None))
+        lib = L.lib()
+        # an older diagnostic library (NINWAVE_LIB, A/B runs) may lack the symbol: no advice then
+        if hasattr(lib, 'nw_host_advise'):
+            L.check(lib.nw_host_advise(ctypes.c_void_p(arr.ctypes.data), int(arr.nbytes), None))
 
     def free_bytes(self) -> int:
         self._drain()
         with self._lock:
             return sum(n * len(v) for n, v in self._free.items())
+
+    def trim(self) -> int:
+        """Free every idle pooled buffer now and return the bytes released.  Buffers come back
+        lazily: a dropped result is filed by the next empty() / free_bytes() / trim(), so up to
+        the cap stays page-locked (and counted in ``held``) after the last result is gone until
+        one of them runs."""
+        self._drain()
+        drop = []
+        with self._lock:
+            for n, lst in self._free.items():
+                while lst:
+                    drop.append((lst.pop(), n))
+                    self.held -= n
+        for ptr, _ in drop:
+            self._free_fn(ptr)
+        return sum(n for _, n in drop)
 
     def _drain(self):
         """File the buffers finalizers returned: keep up to keep_free per size, free the rest
@@ -189,8 +208,23 @@ def default_pool_cap(total_ram: int | None = None, local_ranks: int | None = Non
         except (ValueError, OSError, AttributeError):
             total_ram = 64 << 30
     if local_ranks is None:
-        local_ranks = int(os.environ.get('LOCAL_WORLD_SIZE') or os.environ.get('WORLD_SIZE') or 1)
+        local_ranks = local_rank_count()
     return int(min(8 << 30, total_ram // 8) // max(1, local_ranks))
+
+
+def local_rank_count(env=None) -> int:
+    """Processes of this job on this node: torchrun's LOCAL_WORLD_SIZE, else the launcher's
+    node-local count (Slurm, Open MPI, MPICH/Hydra), else 1.  Never the global WORLD_SIZE: on a
+    multi-node launch that would shrink every rank's pool by the total rank count."""
+    env = os.environ if env is None else env
+    for k in ('LOCAL_WORLD_SIZE', 'SLURM_NTASKS_PER_NODE', 'OMPI_COMM_WORLD_LOCAL_SIZE', 'MPI_LOCALNRANKS'):
+        v = env.get(k)
+        if v:
+            try:
+                return max(1, int(str(v).split('(')[0].split(',')[0]))
+            except ValueError:
+                continue
+    return 1
 
 
 HOST_POOL = HostPool(int(os.environ.get('NINWAVE_HOST_POOL_BYTES') or default_pool_cap()))
@@ -260,6 +294,13 @@ class Plan:
         dt = self.dtype if self.kind not in TABLE_KINDS else out_dtype(self.dtype, 'cwt')
         out = np.empty((self.nfreq, self.grid.len_full), dtype=dt)
         L.check(L.lib().nw_plan_wavelet_rows(self._h, out.ctypes.data_as(ctypes.c_void_p)))
+        return out
+
+    def row_support(self, scan: bool = False) -> np.ndarray:
+        """Two-pass engine diagnostic: each row's last bin above the tail threshold (the row
+        pass's pruning bound, nw_plan_row_support); scan=True by scanning every bin."""
+        out = np.empty(self.nfreq, dtype=np.int32)
+        L.check(L.lib().nw_plan_row_support(self._h, 1 if scan else 0, out.ctypes.data_as(ctypes.c_void_p)))
         return out
 
     # -- execute -----------------------------------------------------------------

@@ -241,28 +241,41 @@ def _plan(n, F, dtype, freqs, engine=None, max_batch=8, kind='morse', params=(17
 @pytest.mark.parametrize('engine', ENGINES)
 @pytest.mark.parametrize('dtype', ['float64', 'float32'])
 def test_epoch_reductions_match_materialised(dtype, engine):
-    """power_mean / itc (mneutils.py:42-71) reduced on the device over 3 chunks equal the
-    reference formulas applied to the materialised CWT of the same plan; the fp64 sum
-    kinds are the un-normalised partials.  Tolerance: 1e-13 (fp64), 2e-6 (fp32: the fused
-    kernel's |y|^2 is rounded to fp32 before the fp64 sum)."""
+    """power_mean / itc (mneutils.py:42-71) reduced on the device over 3 chunks against the
+    reference formulas on the oracle's CWT of the same signals: power 2e-12 (fp64) / 2e-5
+    (fp32) of max, ITC |d| <= 1e-10 (fp64) or INTEGRATION.md's fp32 contract (2e-5 where
+    every epoch's |cwt| >= 0.1 of its row's max, 1e-3 everywhere); the fp64 sum kinds are the
+    un-normalised partials of the same accumulators (power_mean = power_sum / S, itc =
+    |phase_sum| / S, one rounding to the compute dtype), and the materialised CWT of the same
+    plan reduces to the same values within the contract."""
     n, F, S = 4096, 24, 21
     x = synth(S, n, 21).astype(dtype)
     freqs = np.linspace(2., 120., F)
     plan = _plan(n, F, dtype, freqs, engine)
-    c = plan.execute(x, out_kind='cwt').astype(np.complex128)
-    ref_p = np.mean(np.abs(c) ** 2, axis=0)
-    ref_i = np.abs(np.mean(c / np.abs(c), axis=0))
-    t = 1e-13 if dtype == 'float64' else 2e-6
+    o = np.stack([O.cwt('morse', x[s].astype(np.float64), freqs) for s in range(S)])
+    ref_p = np.mean(np.abs(o) ** 2, axis=0)
+    mag = np.abs(o)
+    ref_i = np.abs(np.mean(o / mag, axis=0))
+    good = np.all(mag >= 0.1 * mag.max(axis=-1, keepdims=True), axis=0)
+    f64 = dtype == 'float64'
     pm = plan.execute(x, out_kind='power_mean')
     itc = plan.execute(x, out_kind='itc')
     assert pm.shape == (F, n) and pm.dtype == np.dtype(dtype) and itc.dtype == np.dtype(dtype)
-    assert rel_err(pm, ref_p) <= t
-    assert np.max(np.abs(itc - ref_i)) <= t           # ITC lies in [0, 1]
     ps = plan.execute(x, out_kind='power_sum')
     ph = plan.execute(x, out_kind='phase_sum')
     assert ps.dtype == np.float64 and ph.dtype == np.complex128
-    assert rel_err(ps / S, ref_p) <= t
-    assert np.max(np.abs(np.abs(ph / S) - ref_i)) <= t
+    one = 1e-15 if f64 else 1.2e-7                    # one rounding to the compute dtype
+    assert rel_err(pm, ps / S) <= one
+    assert np.max(np.abs(itc - np.abs(ph) / S)) <= one
+    c = plan.execute(x, out_kind='cwt').astype(np.complex128)
+    for p_, i_ in ((pm, itc), (np.mean(np.abs(c) ** 2, axis=0), np.abs(np.mean(c / np.abs(c), axis=0)))):
+        assert rel_err(p_, ref_p) <= (2e-12 if f64 else 2e-5)
+        d = np.abs(i_.astype(np.float64) - ref_i)
+        if f64:
+            assert d.max() <= 1e-10
+        else:
+            dg = d[good].max() if good.any() else 0.0
+            assert dg <= 2e-5 and d.max() <= 1e-3, (dg, d.max())
 
 
 @pytest.mark.parametrize('engine', ENGINES)

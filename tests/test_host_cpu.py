@@ -331,3 +331,40 @@ def test_default_pool_cap_shares_the_node():
     assert default_pool_cap(1 << 40, 1) == 8 << 30                 # 8 GiB per process
     assert default_pool_cap(1 << 40, 8) == 1 << 30                 # eight ranks of a node: 8 GiB in all
     assert default_pool_cap(16 << 30, 1) == 2 << 30                # at most 1/8 of the host's RAM
+
+
+def test_pool_cap_counts_node_local_ranks_only():
+    """A multi-node launch without LOCAL_WORLD_SIZE: the pool is shared by this node's ranks
+    (the launcher's node-local count), never divided by the global WORLD_SIZE."""
+    from ninwavelets_amd.engine import local_rank_count
+    assert local_rank_count({'WORLD_SIZE': '64', 'RANK': '9'}) == 1
+    assert local_rank_count({'WORLD_SIZE': '64', 'LOCAL_WORLD_SIZE': '8'}) == 8
+    assert local_rank_count({'WORLD_SIZE': '64', 'SLURM_NTASKS_PER_NODE': '8(x8)'}) == 8
+    assert local_rank_count({'WORLD_SIZE': '64', 'OMPI_COMM_WORLD_LOCAL_SIZE': '4'}) == 4
+    assert local_rank_count({'LOCAL_WORLD_SIZE': 'x', 'MPI_LOCALNRANKS': '2'}) == 2
+
+
+def test_pool_trim_frees_idle_buffers():
+    from ninwavelets_amd.engine import HostPool
+    freed = []
+    nxt = iter(range(1, 100))
+    pool = HostPool(cap=1 << 20, min_bytes=1024, keep_free=2, alloc=lambda n: next(nxt) * 4096,
+                    free=freed.append, advise=lambda a: None)
+    a, b = pool.empty((512,), np.float64), pool.empty((256,), np.float64)
+    kept = pool.empty((512,), np.float64)
+    assert pool.held == 4096 + 2048 + 4096
+    del a, b
+    assert pool.trim() == 4096 + 2048 and len(freed) == 2
+    assert pool.held == 4096 and pool.free_bytes() == 0          # the live result stays
+    del kept
+    assert pool.trim() == 4096 and pool.held == 0
+
+
+def test_pool_advice_skipped_without_the_symbol(monkeypatch):
+    """An older diagnostic library without nw_host_advise: over-cap results stay plain arrays."""
+    from ninwavelets_amd import engine
+
+    class OldLib:
+        pass
+    monkeypatch.setattr(engine.L, 'lib', lambda: OldLib())
+    engine.HostPool._nw_advise(np.empty(16))                   # no AttributeError
