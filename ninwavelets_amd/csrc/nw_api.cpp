@@ -150,6 +150,7 @@ const char* const kStageName[ST_N] = {"forward", "multiply", "inverse", "epilogu
 struct Pending {
     int stage;
     hipEvent_t a, b;
+    bool own_a = true;   // false: a is the previous stage's b (chained), released with it
 };
 
 }  // namespace
@@ -254,6 +255,15 @@ int ensure(void** ptr, size_t* cur, size_t want) {
     return NW_OK;
 }
 
+}  // namespace
+
+nw::StageEvents& nw::stage_events() {
+    static thread_local StageEvents se;
+    return se;
+}
+
+namespace {
+
 int take_event(nw_plan* p, hipEvent_t* ev) {
     if (!p->event_pool.empty()) {
         *ev = p->event_pool.back();
@@ -279,18 +289,59 @@ void count_launch(nw_plan* p, int stage) {
     }
 }
 
+// chain = true: the caller enqueued nothing on the stream since the previous staged() call
+// returned, so that stage's end event is this one's start (one event record less per
+// boundary: each costs the stream a few microseconds, 3 % of a C2 step)
 template <typename F>
-int staged(nw_plan* p, int stage, F&& fn) {
+int staged(nw_plan* p, int stage, F&& fn, bool chain = false) {
     count_launch(p, stage);
     nw_logf(2, "plan %p: launch %s%s%s", (void*)p, kStageName[stage], stage == ST_FUSED || stage == ST_ROWS ? ": " : "",
             stage == ST_FUSED || stage == ST_ROWS ? kernel_name(p->stats.kernel) : "");
     if (!(p->flags & NW_TIMING)) return fn();
     Pending pe{stage, nullptr, nullptr};
-    NW_TRY(take_event(p, &pe.a));
+    if (chain && !p->pending.empty()) {
+        pe.a = p->pending.back().b;
+        pe.own_a = false;
+    } else {
+        NW_TRY(take_event(p, &pe.a));
+        NW_HIP(hipEventRecord(pe.a, p->stream));
+    }
     NW_TRY(take_event(p, &pe.b));
-    NW_HIP(hipEventRecord(pe.a, p->stream));
     int r = fn();
     NW_HIP(hipEventRecord(pe.b, p->stream));
+    p->pending.push_back(pe);
+    return r;
+}
+
+// A stage whose work is kernels launched through nw_launch (nw_internal.h): with NW_TIMING
+// its events ride on those launches (hipExtLaunchKernel: the stop event is the last dispatch's
+// own end; the start event is one marker before the first), and a chained stage (the previous
+// stage was the last thing enqueued) starts at that stage's stop, so it adds no marker at all;
+// a stage that launched nothing records both at once (0 ms)
+template <typename F>
+int staged_k(nw_plan* p, int stage, F&& fn, bool chain = false) {
+    if (!(p->flags & NW_TIMING)) return staged(p, stage, fn);
+    count_launch(p, stage);
+    nw_logf(2, "plan %p: launch %s%s%s", (void*)p, kStageName[stage], stage == ST_FUSED || stage == ST_ROWS ? ": " : "",
+            stage == ST_FUSED || stage == ST_ROWS ? kernel_name(p->stats.kernel) : "");
+    Pending pe{stage, nullptr, nullptr};
+    const bool chained = chain && !p->pending.empty();
+    if (chained) {
+        pe.a = p->pending.back().b;
+        pe.own_a = false;
+    } else {
+        NW_TRY(take_event(p, &pe.a));
+    }
+    NW_TRY(take_event(p, &pe.b));
+    nw::StageEvents& se = nw::stage_events();
+    se = nw::StageEvents{chained ? nullptr : pe.a, pe.b, 0};
+    const int r = fn();
+    const int launched = se.launches;
+    se = nw::StageEvents{};
+    if (launched == 0) {
+        if (!chained) NW_HIP(hipEventRecord(pe.a, p->stream));
+        NW_HIP(hipEventRecord(pe.b, p->stream));
+    }
     p->pending.push_back(pe);
     return r;
 }
@@ -312,7 +363,7 @@ int resolve_timing(nw_plan* p) {
             case ST_EXPAND: p->stats.ms_expand += ms; break;
             default: p->stats.ms_copy += ms; break;
         }
-        p->event_pool.push_back(pe.a);
+        if (pe.own_a) p->event_pool.push_back(pe.a);
         p->event_pool.push_back(pe.b);
     }
     p->pending.clear();
@@ -486,7 +537,7 @@ int run_overflow_rows(nw_plan* p, int64_t c, void* dst, int out_kind) {
     const size_t ybytes = (size_t)c * U * crow;
     NW_TRY(ensure(&p->d_oscr, &p->d_oscr_bytes, ybytes + (out_kind == NW_OUT_CWT ? 0 : (size_t)c * U * orow)));
     char* Y = (char*)p->d_oscr;
-    NW_TRY(staged(p, ST_MUL, [&] {
+    NW_TRY(staged_k(p, ST_MUL, [&] {
         NW_HIP(nw::launch_multiply(od, p->dtype, p->d_X, Y, c, p->stream));
         return NW_OK;
     }));
@@ -494,7 +545,7 @@ int run_overflow_rows(nw_plan* p, int64_t c, void* dst, int out_kind) {
     const char* src = Y;
     if (out_kind != NW_OUT_CWT) {
         char* Z = Y + ybytes;
-        NW_TRY(staged(p, ST_EPI, [&] {
+        NW_TRY(staged_k(p, ST_EPI, [&] {
             NW_HIP(nw::launch_epilogue(p->dtype, out_kind, Y, Z, c * U * p->n, p->stream));
             return NW_OK;
         }));
@@ -502,7 +553,7 @@ int run_overflow_rows(nw_plan* p, int64_t c, void* dst, int out_kind) {
     }
     const int32_t* hb = (const int32_t*)p->d_obuf;
     const size_t o_offs = ((size_t)U * 4 + 15) / 16 * 16, o_order = o_offs + ((size_t)(U + 1) * 4 + 15) / 16 * 16;
-    return staged(p, ST_EXPAND, [&] {
+    return staged_k(p, ST_EXPAND, [&] {
         NW_HIP(nw::launch_expand_rows(src, dst, c, U, p->nfreq, orow, hb + o_offs / 4, hb + o_order / 4, p->stream));
         return NW_OK;
     });
@@ -514,9 +565,13 @@ constexpr int OUT_PHSUM = 1002;   // complex fp64 phase partials (y / |y|)
 int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind, bool dst_is_final) {
     bool rocfft_engine = p->engine == NW_ENGINE_ROCFFT;
     // fused sizes: the forward R2C by nw_fused.hip's fwd_r2c_kernel (no copy, one kernel)
+    // the forward stage was the last thing enqueued (the fused form's launch may chain onto it)
+    bool fwd_chain = false;
+    const bool table_was_valid = p->wtab_valid;
     if (!rocfft_engine && !p->large && !p->chirp) {
         // power-of-two n <= 16384: the on-chip forward transform reads the caller's rows directly
-        NW_TRY(staged(p, ST_FWD, [&] {
+        fwd_chain = true;
+        NW_TRY(staged_k(p, ST_FWD, [&] {
             NW_HIP(nw::fused_forward(p->n, p->dtype, xs_dev, p->d_X, c, p->nh, p->stream));
             return NW_OK;
         }));
@@ -549,20 +604,20 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
         for (int64_t sidx = 0; sidx < c; ++sidx) {
             const char* Xs = (const char*)p->d_X + (size_t)sidx * p->nh * 2 * p->esz;
             char* os = (char*)dst + (size_t)sidx * p->nfreq * out_row;
-            NW_TRY(staged(p, ST_COPY, [&] {   // the spectrum transpose: timed with the copies
+            NW_TRY(staged_k(p, ST_COPY, [&] {   // the spectrum transpose: timed with the copies
                 NW_HIP(nw::large_transpose(p->desc, p->dtype, Xs, p->d_scratch, p->stream));
                 return NW_OK;
             }));
             for (int64_t f0 = 0; f0 < p->nfreq; f0 += fc) {
                 const int nf = (int)std::min<int64_t>(fc, p->nfreq - f0);
-                NW_TRY(staged(p, ST_ROWS, [&] {
+                NW_TRY(staged_k(p, ST_ROWS, [&] {
                     NW_HIP(nw::large_rows(p->desc, p->dtype, (int)f0, nf, p->d_wtab, p->d_scratch, p->stream));
                     return NW_OK;
-                }));
-                NW_TRY(staged(p, ST_FUSED, [&] {
+                }, true));
+                NW_TRY(staged_k(p, ST_FUSED, [&] {
                     NW_HIP(nw::large_cols(p->desc, p->dtype, out_kind, (int)f0, nf, p->d_wtab, p->d_scratch, os, p->stream));
                     return NW_OK;
-                }));
+                }, true));
             }
         }
         return NW_OK;
@@ -572,7 +627,7 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
         NW_TRY(chirp_table(p));
         p->stats.kernel = NW_K_CHIRP;
         if (p->chirp) {
-            NW_TRY(staged(p, ST_FUSED, [&] {
+            NW_TRY(staged_k(p, ST_FUSED, [&] {
                 NW_HIP(nw::launch_chirp(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->chirp_counts,
                                         p->stream));
                 return NW_OK;
@@ -591,17 +646,17 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
         }
         if (out_kind == OUT_PSUM || out_kind == OUT_PHSUM) {
             p->stats.kernel = nw::fused_psum_kernel_id(p->n, p->dtype, out_kind == OUT_PHSUM);
-            return staged(p, ST_FUSED, [&] {
+            return staged_k(p, ST_FUSED, [&] {
                 NW_HIP(nw::fused_power_partials(p->desc, p->dtype, out_kind == OUT_PHSUM, p->d_X, p->d_wtab, dst, c,
                                                 p->stream));
                 return NW_OK;
             });
         }
         p->stats.kernel = nw::fused_kernel_id(p->n, p->dtype, p->desc.kind);
-        return staged(p, ST_FUSED, [&] {
+        return staged_k(p, ST_FUSED, [&] {
             NW_HIP(nw::launch_fused(p->desc, p->dtype, out_kind, p->d_X, p->d_wtab, dst, c, p->stream));
             return NW_OK;
-        });
+        }, fwd_chain && table_was_valid);
     }
     // K1 writes the product straight into the destination when the caller wants
     // the complex CWT on the device; otherwise into the plan's Y buffer.
@@ -611,7 +666,7 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
         Y = p->d_Y;
     }
     p->stats.kernel = NW_K_MULTIPLY;
-    NW_TRY(staged(p, ST_MUL, [&] {
+    NW_TRY(staged_k(p, ST_MUL, [&] {
         NW_HIP(nw::launch_multiply(p->desc, p->dtype, p->d_X, Y, c, p->stream));
         return NW_OK;
     }));
@@ -628,7 +683,7 @@ int run_chunk_rows(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out
             }));
         return NW_OK;
     }
-    return staged(p, ST_EPI, [&] {
+    return staged_k(p, ST_EPI, [&] {
         NW_HIP(nw::launch_epilogue(p->dtype, out_kind, Y, dst, c * p->nfreq * p->n, p->stream));
         return NW_OK;
     });
@@ -667,11 +722,11 @@ int run_chunk(nw_plan* p, const void* xs_dev, int64_t c, void* dst, int out_kind
         UniqueRows u(p);   // d_uout is scratch of the CWT's row size: K1 may write it
         NW_TRY(run_chunk_rows(p, xs_dev, c, p->d_uout, out_kind, true));
     }
-    return staged(p, ST_EXPAND, [&] {
+    return staged_k(p, ST_EXPAND, [&] {   // run_chunk_rows ends with a staged stage: chain onto it
         NW_HIP(nw::launch_expand_rows(p->d_uout, dst, crows, p->nuniq, p->nfreq, row, p->d_rep, p->d_rep + p->nuniq + 1,
                                       p->stream));
         return NW_OK;
-    });
+    }, true);
 }
 
 bool is_reduction(int out_kind) { return out_kind >= NW_OUT_POWER_MEAN && out_kind <= NW_OUT_PHASE_SUM; }
@@ -733,12 +788,12 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
             xs = p->d_x;
         }
         NW_TRY(run_chunk(p, xs, c, scratch, sig_kind, false));
-        NW_TRY(staged(p, ST_EPI, [&] {
+        NW_TRY(staged_k(p, ST_EPI, [&] {   // chained: run_chunk ends with a staged stage
             const int64_t rows = psum ? nw::fused_psum_groups(c) : c;
             NW_HIP(nw::launch_accumulate(psum ? NW_F64 : p->dtype, src_kind, scratch, (double*)p->d_acc,
                                          psum && phase ? 2 * fn : fn, rows, p->stream));
             return NW_OK;
-        }));
+        }, true));
         p->stats.chunks++;
     }
     const hipMemcpyKind back = host ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
@@ -747,7 +802,7 @@ int execute_reduce(nw_plan* p, const void* x, int64_t nsig, void* out, int out_k
     } else {
         // scratch is >= fn elements of the plan dtype on both engines
         void* dst = host ? scratch : out;
-        NW_TRY(staged(p, ST_EPI, [&] {
+        NW_TRY(staged_k(p, ST_EPI, [&] {
             NW_HIP(nw::launch_finalize(p->dtype, phase, (const double*)p->d_acc, dst, fn, nsig, p->stream));
             return NW_OK;
         }));

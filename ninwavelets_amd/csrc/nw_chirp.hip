@@ -345,10 +345,10 @@ hipError_t chirp_tables(int64_t n, int64_t m, int dtype, void** out) {
     if (e != hipSuccess) return e;
     const unsigned bm = (unsigned)((m + 255) / 256), bn = (unsigned)((n + 255) / 256);
     if (dtype == NW_F32) {
-        chirp_bhat_kernel<float><<<bm, 256>>>((C2<float>*)p, (int)n, (int)m);
+        hipLaunchKernelGGL(chirp_bhat_kernel<float>, bm, 256, 0, 0, (C2<float>*)p, (int)n, (int)m);
     } else {
-        chirp_bhat_kernel<double><<<bm, 256>>>((C2<double>*)p, (int)n, (int)m);
-        chirp_ct_kernel<double><<<bn, 256>>>((C2<double>*)p + m, (int)n);
+        hipLaunchKernelGGL(chirp_bhat_kernel<double>, bm, 256, 0, 0, (C2<double>*)p, (int)n, (int)m);
+        hipLaunchKernelGGL(chirp_ct_kernel<double>, bn, 256, 0, 0, (C2<double>*)p + m, (int)n);
     }
     e = hipGetLastError();
     if (e == hipSuccess) e = hipDeviceSynchronize();
@@ -384,7 +384,7 @@ hipError_t launch_m_e(const WDesc& d, int out_kind, const void* X, const void* w
     auto go = [&](auto kern) {
         e = hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return;
-        kern<<<(unsigned)blocks, threads, lds, s>>>(d, Xc, wtab, out, twc, bh, ct, nsig, (int)nsg_pad, rowmap, nrows,
+        nw_launch(kern, (unsigned)blocks, threads, lds, s, d, Xc, wtab, out, twc, bh, ct, nsig, (int)nsg_pad, rowmap, nrows,
                                                     ksup);
         e = hipGetLastError();
     };
@@ -452,15 +452,15 @@ hipError_t build_chirp_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t
     int* ksup = reinterpret_cast<int*>(reinterpret_cast<char*>(wtab) + chirp_w_bytes(d.n, d.nfreq, dtype, d.kind));
     int* rowmap = ksup + d.nfreq;
     if (dtype == NW_F32) {
-        if (realw) chirp_wtable_kernel<float, true><<<grid, 256, 0, s>>>(d, wtab);
-        else chirp_wtable_kernel<float, false><<<grid, 256, 0, s>>>(d, wtab);
-        if (realw) chirp_support_kernel<float, true><<<d.nfreq, 256, 0, s>>>(wtab, d.n, ksup);
-        else chirp_support_kernel<float, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, ksup);
+        if (realw) nw_launch(chirp_wtable_kernel<float, true>, grid, 256, 0, s, d, wtab);
+        else nw_launch(chirp_wtable_kernel<float, false>, grid, 256, 0, s, d, wtab);
+        if (realw) nw_launch(chirp_support_kernel<float, true>, d.nfreq, 256, 0, s, wtab, d.n, ksup);
+        else nw_launch(chirp_support_kernel<float, false>, d.nfreq, 256, 0, s, wtab, d.n, ksup);
     } else {
-        if (realw) chirp_wtable_kernel<double, true><<<grid, 256, 0, s>>>(d, wtab);
-        else chirp_wtable_kernel<double, false><<<grid, 256, 0, s>>>(d, wtab);
-        if (realw) chirp_support_kernel<double, true><<<d.nfreq, 256, 0, s>>>(wtab, d.n, ksup);
-        else chirp_support_kernel<double, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, ksup);
+        if (realw) nw_launch(chirp_wtable_kernel<double, true>, grid, 256, 0, s, d, wtab);
+        else nw_launch(chirp_wtable_kernel<double, false>, grid, 256, 0, s, d, wtab);
+        if (realw) nw_launch(chirp_support_kernel<double, true>, d.nfreq, 256, 0, s, wtab, d.n, ksup);
+        else nw_launch(chirp_support_kernel<double, false>, d.nfreq, 256, 0, s, wtab, d.n, ksup);
     }
     hipError_t e = hipGetLastError();
     // once per wavelet: the rows' M classes on the host (M >= n + K - 1 wrap-free, >= 2K for

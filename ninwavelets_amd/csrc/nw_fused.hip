@@ -16,6 +16,7 @@
 //   dst[(j / Ns) * Ns * R + (j mod Ns) + r * Ns] = v[r]
 // IDFT_R is a radix-2 decimation-in-frequency network in registers whose output
 // comes out bit-reversed; stores index it with bitrev(i) (compile-time, free).
+#include <cstdlib>
 #include <map>
 #include <mutex>
 #include <tuple>
@@ -88,8 +89,12 @@ constexpr bool kPairXD = true;
 template <typename T, int N, int E> constexpr bool kNz24Of = kNz24 && E > 16;
 // NZ = 12 and 20 between them (fp32 only: fp64 n = 16384 |y| spills 20 B with them)
 template <typename T, int N, int E> constexpr bool kNzFineOf = kNz24Of<T, N, E> && sizeof(T) == 4;
-// ... and for the fp64 cwt output (-DNW_F64_FINE: diagnostic A/B; its |y| spills with them)
-#ifdef NW_F64_FINE
+// ... and for the fp64 cwt output (round 6: C4 shape fp64 -0.7 to -0.9 %; its |y| spills with
+// them; -DNW_F64_FINE=0 for the A/B)
+#ifndef NW_F64_FINE
+#define NW_F64_FINE 1
+#endif
+#if NW_F64_FINE
 template <typename T, int N, int E, int OUT> constexpr bool kNzFineOut = kNzFineOf<T, N, E> ||
     (kNz24Of<T, N, E> && OUT == NW_OUT_CWT);
 #else
@@ -109,15 +114,15 @@ __device__ __forceinline__ int pass0_variant(int nz) {
     return E;
 }
 // signals per block: C3 0.354 -> 0.348 ms, C4 1.774 -> 1.770 vs 4 (2 and 16 slower or equal).
-// fp64 (one block per CU) takes 4: an XCD round of 8 scales x 4 groups then reads W (8 x 128
-// KiB) + X (16 x 128 KiB) = 3 MiB, inside the XCD's 4 MiB L2 (8 signals: 5 MiB, re-read from
-// the Infinity Cache); the C4 shape in fp64 10.04 -> 9.66 ms per launch (2 / 3 signals:
-// 9.55 / 9.40, 16: 9.71; two boxes, tools/ab.sh)
+// fp64 (one block per CU): 8 since round 6 (C4 shape fp64 7.31-7.32 -> 7.25-7.28 ms per launch,
+// with the fine pass-0 variants below 7.21-7.24; 2 signals +2.6 %, tiles 4 x 8 +1.5 %, 8 x 2
+// +0.3 %; profiles/r06_f64_group_ab.txt).  Round 3 had taken 4 (then 10.04 -> 9.66 ms against
+// 8 signals, when X was re-read from L2 per scale without the LDS-DMA)
 constexpr int kGroup = 8;
 static_assert(kGroup == kPsumGroup, "fused partial rows are counted by fused_psum_groups");
 // (-DNW_GROUP64 / NW_TILE64_F / NW_TILE64_G: diagnostic A/B of the fp64 block and tile shape)
 #ifndef NW_GROUP64
-#define NW_GROUP64 4
+#define NW_GROUP64 8
 #endif
 constexpr int kGroup64 = NW_GROUP64;
 // XCD tile: kTileF scales x kTileG signal groups per XCD round (fp64 tiles 16 x 2, 4 x 8,
@@ -629,9 +634,9 @@ hipError_t twiddles_for(int64_t n, int dtype, void** out) {
     e = hipMalloc(&p, (size_t)n * esz);
     if (e != hipSuccess) return e;
     if (dtype == NW_F32)
-        twiddle_table_kernel<float><<<(unsigned)((n + 255) / 256), 256>>>((C2<float>*)p, (int)n);
+        hipLaunchKernelGGL(twiddle_table_kernel<float>, (unsigned)((n + 255) / 256), 256, 0, 0, (C2<float>*)p, (int)n);
     else
-        twiddle_table_kernel<double><<<(unsigned)((n + 255) / 256), 256>>>((C2<double>*)p, (int)n);
+        hipLaunchKernelGGL(twiddle_table_kernel<double>, (unsigned)((n + 255) / 256), 256, 0, 0, (C2<double>*)p, (int)n);
     e = hipGetLastError();
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
@@ -653,7 +658,7 @@ hipError_t launch_forward(const void* x, void* X, int64_t nsig, int64_t nh, hipS
     e = hipFuncSetAttribute((const void*)fwd_r2c_kernel<T, N, E>, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     if (nsig > 0x7fffffff) return hipErrorInvalidConfiguration;
-    fwd_r2c_kernel<T, N, E><<<(unsigned)nsig, N / E, lds, s>>>(reinterpret_cast<const T*>(x), reinterpret_cast<C2<T>*>(X),
+    nw_launch(fwd_r2c_kernel<T, N, E>, (unsigned)nsig, N / E, lds, s, reinterpret_cast<const T*>(x), reinterpret_cast<C2<T>*>(X),
                                                              reinterpret_cast<const C2<T>*>(tw), nh);
     return hipGetLastError();
 }
@@ -667,6 +672,22 @@ size_t wtab_row_bytes(int64_t n, int nfreq, size_t esz, bool realw) {
 template <typename T, int E, bool REALW>
 constexpr bool kPairMode = std::is_same<T, float>::value && E <= 16 && REALW;
 
+// Signals per block of the output kernels: `base`, halved (to 2) while a launch would fill the
+// chip fewer than kMinRounds times over (512 resident 512-thread blocks): a small launch (C2:
+// 64 signals x 128 scales = 1024 blocks of 8, two rounds) otherwise ends on a tail of long
+// blocks.  NW_FUSED_GROUP=<g> fixes it (diagnostic A/B).
+constexpr int64_t kMinRounds = 4, kResidentBlocks = 512;
+int group_for(int base, int64_t nsig, int nfreq) {
+    static const int fixed = [] {
+        const char* v = std::getenv("NW_FUSED_GROUP");
+        return v ? std::atoi(v) : 0;
+    }();
+    if (fixed > 0) return fixed;
+    int g = base;
+    while (g > 2 && (nsig + g - 1) / g * (int64_t)nfreq < kMinRounds * kResidentBlocks) g /= 2;
+    return g;
+}
+
 template <typename T, int N, int E, bool REALW>
 hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wtab, void* out, int64_t nsig,
                     hipStream_t s) {
@@ -675,7 +696,7 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
-    const int grp = sizeof(T) == 8 ? kGroup64 : kGroup;
+    const int grp = kPairMode<T, E, REALW> ? kGroup : group_for(sizeof(T) == 8 ? kGroup64 : kGroup, nsig, d.nfreq);
     const int64_t nsg = (nsig + grp - 1) / grp;
     constexpr int TF = kTileFT<T>;
     const int TG = tile_g_of(nsg, kTileGT<T>);
@@ -692,19 +713,19 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
         const C2<float>* twf = reinterpret_cast<const C2<float>*>(tw);
         const cplx<float>* Xf = reinterpret_cast<const cplx<float>*>(X);
         if (out_kind == NW_OUT_CWT)
-            nw_fused_pair_kernel<N, E, NW_OUT_CWT><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
+            nw_launch(nw_fused_pair_kernel<N, E, NW_OUT_CWT>, blocks, threads, lp, s, d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
         else if (out_kind == NW_OUT_POWER)
-            nw_fused_pair_kernel<N, E, NW_OUT_POWER><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
+            nw_launch(nw_fused_pair_kernel<N, E, NW_OUT_POWER>, blocks, threads, lp, s, d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
         else
-            nw_fused_pair_kernel<N, E, NW_OUT_ABS><<<blocks, threads, lp, s>>>(d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
+            nw_launch(nw_fused_pair_kernel<N, E, NW_OUT_ABS>, blocks, threads, lp, s, d, Xf, wtab, out, twf, nsig, kGroup, (int)nsg_pad, wnz, TG);
         return hipGetLastError();
     }
     if (out_kind == NW_OUT_CWT)
-        nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
+        nw_launch(nw_fused_kernel<T, N, E, NW_OUT_CWT, REALW>, blocks, threads, lds, s, d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
     else if (out_kind == NW_OUT_POWER)
-        nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
+        nw_launch(nw_fused_kernel<T, N, E, NW_OUT_POWER, REALW>, blocks, threads, lds, s, d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
     else
-        nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW><<<blocks, threads, lds, s>>>(d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
+        nw_launch(nw_fused_kernel<T, N, E, NW_OUT_ABS, REALW>, blocks, threads, lds, s, d, Xc, wtab, out, twc_, nsig, grp, (int)nsg_pad, wnz, TG);
     return hipGetLastError();
 }
 
@@ -733,12 +754,12 @@ hipError_t launch_psum(const WDesc& d, const void* X, const void* wtab, void* pa
         e = hipFuncSetAttribute((const void*)nw_fused_pair_kernel<N, E, kOutPSum>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, lp);
         if (e != hipSuccess) return e;
-        nw_fused_pair_kernel<N, E, kOutPSum><<<blocks, threads, lp, s>>>(
+        nw_launch(nw_fused_pair_kernel<N, E, kOutPSum>, blocks, threads, lp, s, 
             d, reinterpret_cast<const cplx<float>*>(X), wtab, partials, reinterpret_cast<const C2<float>*>(tw), nsig,
             kGroup, (int)nsg_pad, wnz, TG);
         return hipGetLastError();
     }
-    nw_fused_kernel<T, N, E, OUT, true, WSH><<<blocks, threads, lds, s>>>(
+    nw_launch(nw_fused_kernel<T, N, E, OUT, true, WSH>, blocks, threads, lds, s, 
         d, reinterpret_cast<const cplx<T>*>(X), wtab, partials, reinterpret_cast<const C2<T>*>(tw), nsig, kGroup,
         (int)nsg_pad, wnz, TG);
     return hipGetLastError();
@@ -825,15 +846,15 @@ hipError_t build_wtable(const WDesc& d, int dtype, void* wtab, hipStream_t s) {
     if (e == 0) return hipErrorNotSupported;
     const int tt = (int)(d.n / e);
     if (dtype == NW_F32) {
-        if (realw) wtable_kernel<float, true><<<grid, 256, 0, s>>>(d, wtab);
-        else wtable_kernel<float, false><<<grid, 256, 0, s>>>(d, wtab);
-        if (realw) wsupport_kernel<float, true><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
-        else wsupport_kernel<float, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
+        if (realw) nw_launch(wtable_kernel<float, true>, grid, 256, 0, s, d, wtab);
+        else nw_launch(wtable_kernel<float, false>, grid, 256, 0, s, d, wtab);
+        if (realw) nw_launch(wsupport_kernel<float, true>, d.nfreq, 256, 0, s, wtab, d.n, tt, e, wnz);
+        else nw_launch(wsupport_kernel<float, false>, d.nfreq, 256, 0, s, wtab, d.n, tt, e, wnz);
     } else {
-        if (realw) wtable_kernel<double, true><<<grid, 256, 0, s>>>(d, wtab);
-        else wtable_kernel<double, false><<<grid, 256, 0, s>>>(d, wtab);
-        if (realw) wsupport_kernel<double, true><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
-        else wsupport_kernel<double, false><<<d.nfreq, 256, 0, s>>>(wtab, d.n, tt, e, wnz);
+        if (realw) nw_launch(wtable_kernel<double, true>, grid, 256, 0, s, d, wtab);
+        else nw_launch(wtable_kernel<double, false>, grid, 256, 0, s, d, wtab);
+        if (realw) nw_launch(wsupport_kernel<double, true>, d.nfreq, 256, 0, s, wtab, d.n, tt, e, wnz);
+        else nw_launch(wsupport_kernel<double, false>, d.nfreq, 256, 0, s, wtab, d.n, tt, e, wnz);
     }
     return hipGetLastError();
 }

@@ -1,6 +1,7 @@
 // nw_internal.h — types shared by the C ABI (nw_api.cpp) and the gfx950 kernels.
 #pragma once
 
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -47,6 +48,29 @@ struct WDesc {
 };
 
 template <typename T> struct cplx { T re, im; };
+
+// Timed launches (NW_TIMING): staged() (nw_api.cpp) hands the two events of a stage to the
+// kernel launches the stage makes through nw_launch -- the first launch takes the start event,
+// every launch the stop event -- and hipExtLaunchKernel stamps them with the dispatch's own
+// begin / end (no marker packets between the kernels: recorded with hipEventRecord, the two
+// markers around each launch cost a C2 step 10 %).  Other launches run untimed.
+struct StageEvents {
+    hipEvent_t start = nullptr, stop = nullptr;
+    int launches = 0;
+};
+StageEvents& stage_events();   // thread-local
+
+template <typename K, typename... Args>
+inline void nw_launch(K kernel, dim3 grid, dim3 block, size_t lds, hipStream_t s, Args... args) {
+    StageEvents& se = stage_events();
+    if (se.stop) {
+        hipExtLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, se.start, se.stop, 0u, args...);
+        se.start = nullptr;
+        ++se.launches;
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, (uint32_t)lds, s, args...);
+    }
+}
 
 // ---------------------------------------------------------------------------
 // Analytic spectra.  fp64 follows the reference expression order exactly;

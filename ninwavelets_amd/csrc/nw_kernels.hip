@@ -68,11 +68,11 @@ hipError_t launch_multiply(const WDesc& d, int dtype, const void* X, void* Y, in
               (unsigned)((nsig + K1_GROUP - 1) / K1_GROUP));
     if (dtype == NW_F32) {
         if (d.n % 2 == 0)
-            k1_multiply<float, 2, true><<<grid, K1_THREADS, 0, s>>>(d, (const cplx<float>*)X, (cplx<float>*)Y, nsig);
+            nw_launch(k1_multiply<float, 2, true>, grid, K1_THREADS, 0, s, d, (const cplx<float>*)X, (cplx<float>*)Y, nsig);
         else
-            k1_multiply<float, 2, false><<<grid, K1_THREADS, 0, s>>>(d, (const cplx<float>*)X, (cplx<float>*)Y, nsig);
+            nw_launch(k1_multiply<float, 2, false>, grid, K1_THREADS, 0, s, d, (const cplx<float>*)X, (cplx<float>*)Y, nsig);
     } else {
-        k1_multiply<double, 1, true><<<grid, K1_THREADS, 0, s>>>(d, (const cplx<double>*)X, (cplx<double>*)Y, nsig);
+        nw_launch(k1_multiply<double, 1, true>, grid, K1_THREADS, 0, s, d, (const cplx<double>*)X, (cplx<double>*)Y, nsig);
     }
     return hipGetLastError();
 }
@@ -94,14 +94,14 @@ hipError_t launch_epilogue(int dtype, int out_kind, const void* Y, void* out, in
     const int64_t blocks = std::min<int64_t>((count + 255) / 256, 256 * 16);
     if (dtype == NW_F32) {
         if (out_kind == NW_OUT_POWER)
-            k2_epilogue<float, true><<<blocks, 256, 0, s>>>((const cplx<float>*)Y, (float*)out, count);
+            nw_launch(k2_epilogue<float, true>, blocks, 256, 0, s, (const cplx<float>*)Y, (float*)out, count);
         else
-            k2_epilogue<float, false><<<blocks, 256, 0, s>>>((const cplx<float>*)Y, (float*)out, count);
+            nw_launch(k2_epilogue<float, false>, blocks, 256, 0, s, (const cplx<float>*)Y, (float*)out, count);
     } else {
         if (out_kind == NW_OUT_POWER)
-            k2_epilogue<double, true><<<blocks, 256, 0, s>>>((const cplx<double>*)Y, (double*)out, count);
+            nw_launch(k2_epilogue<double, true>, blocks, 256, 0, s, (const cplx<double>*)Y, (double*)out, count);
         else
-            k2_epilogue<double, false><<<blocks, 256, 0, s>>>((const cplx<double>*)Y, (double*)out, count);
+            nw_launch(k2_epilogue<double, false>, blocks, 256, 0, s, (const cplx<double>*)Y, (double*)out, count);
     }
     return hipGetLastError();
 }
@@ -126,9 +126,9 @@ __global__ __launch_bounds__(256) void k_rows(WDesc d, T* __restrict__ rows) {
 hipError_t launch_rows(const WDesc& d, int dtype, void* rows, hipStream_t s) {
     dim3 grid((unsigned)((d.len_full + 255) / 256), (unsigned)d.nfreq);
     if (dtype == NW_F32)
-        k_rows<float><<<grid, 256, 0, s>>>(d, (float*)rows);
+        nw_launch(k_rows<float>, grid, 256, 0, s, d, (float*)rows);
     else
-        k_rows<double><<<grid, 256, 0, s>>>(d, (double*)rows);
+        nw_launch(k_rows<double>, grid, 256, 0, s, d, (double*)rows);
     return hipGetLastError();
 }
 
@@ -177,9 +177,9 @@ hipError_t launch_accumulate(int dtype, int src_kind, const void* src, double* a
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((fn + 255) / 256, 256 * 32));
 #define NW_ACC(T)                                                                                         \
     switch (src_kind) {                                                                                   \
-        case ACC_POWER_REAL: k_accumulate<T, ACC_POWER_REAL><<<blocks, 256, 0, s>>>(src, acc, fn, c); break; \
-        case ACC_POWER_Y: k_accumulate<T, ACC_POWER_Y><<<blocks, 256, 0, s>>>(src, acc, fn, c); break;       \
-        default: k_accumulate<T, ACC_PHASE_Y><<<blocks, 256, 0, s>>>(src, acc, fn, c); break;               \
+        case ACC_POWER_REAL: nw_launch(k_accumulate<T, ACC_POWER_REAL>, blocks, 256, 0, s, src, acc, fn, c); break; \
+        case ACC_POWER_Y: nw_launch(k_accumulate<T, ACC_POWER_Y>, blocks, 256, 0, s, src, acc, fn, c); break;       \
+        default: nw_launch(k_accumulate<T, ACC_PHASE_Y>, blocks, 256, 0, s, src, acc, fn, c); break;               \
     }
     if (dtype == NW_F32) {
         NW_ACC(float)
@@ -208,11 +208,11 @@ hipError_t launch_finalize(int dtype, bool itc, const double* acc, void* out, in
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((fn + 255) / 256, 256 * 32));
     const double d = (double)nsig;
     if (dtype == NW_F32) {
-        if (itc) k_finalize<float, true><<<blocks, 256, 0, s>>>(acc, (float*)out, fn, d);
-        else k_finalize<float, false><<<blocks, 256, 0, s>>>(acc, (float*)out, fn, d);
+        if (itc) nw_launch(k_finalize<float, true>, blocks, 256, 0, s, acc, (float*)out, fn, d);
+        else nw_launch(k_finalize<float, false>, blocks, 256, 0, s, acc, (float*)out, fn, d);
     } else {
-        if (itc) k_finalize<double, true><<<blocks, 256, 0, s>>>(acc, (double*)out, fn, d);
-        else k_finalize<double, false><<<blocks, 256, 0, s>>>(acc, (double*)out, fn, d);
+        if (itc) nw_launch(k_finalize<double, true>, blocks, 256, 0, s, acc, (double*)out, fn, d);
+        else nw_launch(k_finalize<double, false>, blocks, 256, 0, s, acc, (double*)out, fn, d);
     }
     return hipGetLastError();
 }
@@ -226,7 +226,7 @@ __global__ __launch_bounds__(256) void k_add_f64(double* __restrict__ acc, const
 
 hipError_t launch_add_f64(double* acc, const double* src, int64_t count, hipStream_t s) {
     const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((count + 255) / 256, 256 * 32));
-    k_add_f64<<<blocks, 256, 0, s>>>(acc, src, count);
+    nw_launch(k_add_f64, blocks, 256, 0, s, acc, src, count);
     return hipGetLastError();
 }
 
@@ -263,7 +263,7 @@ __global__ __launch_bounds__(256) void k_normal_time(const NormalRow* __restrict
 
 hipError_t launch_normal_time(const NormalRow* rows, int nrows, int64_t, int kind, double sigma, void* buf,
                               hipStream_t s) {
-    if (nrows > 0) k_normal_time<<<nrows, 256, 0, s>>>(rows, kind, sigma, (double2*)buf);
+    if (nrows > 0) nw_launch(k_normal_time, nrows, 256, 0, s, rows, kind, sigma, (double2*)buf);
     return hipGetLastError();
 }
 
@@ -289,9 +289,9 @@ hipError_t launch_normal_finish(const NormalRow* rows, int nrows, int64_t lmax, 
                                 int dtype, void* table, hipStream_t s) {
     if (nrows > 0) {
         if (dtype == NW_F32)
-            k_normal_finish<float><<<nrows, 256, 0, s>>>(rows, lmax, interp, (const double2*)buf, (cplx<float>*)table);
+            nw_launch(k_normal_finish<float>, nrows, 256, 0, s, rows, lmax, interp, (const double2*)buf, (cplx<float>*)table);
         else
-            k_normal_finish<double><<<nrows, 256, 0, s>>>(rows, lmax, interp, (const double2*)buf, (cplx<double>*)table);
+            nw_launch(k_normal_finish<double>, nrows, 256, 0, s, rows, lmax, interp, (const double2*)buf, (cplx<double>*)table);
     }
     return hipGetLastError();
 }
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(256) void k_wavelet_spectra(const WaveRow* __restri
 }
 
 hipError_t launch_wavelet_spectra(const WaveRow* rows, int nrows, WaveParams wp, void* buf, hipStream_t s) {
-    if (nrows > 0) k_wavelet_spectra<<<nrows, 256, 0, s>>>(rows, wp, (double2*)buf);
+    if (nrows > 0) nw_launch(k_wavelet_spectra, nrows, 256, 0, s, rows, wp, (double2*)buf);
     return hipGetLastError();
 }
 
@@ -348,7 +348,7 @@ __global__ __launch_bounds__(256) void k_wavelet_pack(const WaveRow* __restrict_
 
 hipError_t launch_wavelet_pack(const WaveRow* rows, int nrows, int64_t maxlen, const void* buf, void* out,
                                hipStream_t s) {
-    if (nrows > 0) k_wavelet_pack<<<nrows, 256, 0, s>>>(rows, maxlen, (const double2*)buf, (double2*)out);
+    if (nrows > 0) nw_launch(k_wavelet_pack, nrows, 256, 0, s, rows, maxlen, (const double2*)buf, (double2*)out);
     return hipGetLastError();
 }
 
@@ -376,7 +376,7 @@ __global__ __launch_bounds__(256) void k_wavelet_time(const WaveRow* __restrict_
 
 hipError_t launch_wavelet_time(const WaveRow* rows, int nrows, int64_t maxlen, WaveParams wp, void* out,
                                hipStream_t s) {
-    if (nrows > 0) k_wavelet_time<<<nrows, 256, 0, s>>>(rows, maxlen, wp, (double2*)out);
+    if (nrows > 0) nw_launch(k_wavelet_time, nrows, 256, 0, s, rows, maxlen, wp, (double2*)out);
     return hipGetLastError();
 }
 
@@ -461,17 +461,17 @@ hipError_t launch_baseline(int dtype, const void* x, int64_t count, int64_t b0, 
     const int nb = (int)std::max<int64_t>(1, std::min<int64_t>(BL_BLOCKS, (n + BL_THREADS - 1) / BL_THREADS));
     const int64_t ab = std::max<int64_t>(1, std::min<int64_t>((count + 255) / 256, 256 * 32));
     if (dtype == NW_F32) {
-        k_bl_partial<float, 0><<<nb, BL_THREADS, 0, s>>>((const float*)x, b0, b1, stats, part);
-        k_bl_final<0><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
-        k_bl_partial<float, 1><<<nb, BL_THREADS, 0, s>>>((const float*)x, b0, b1, stats, part);
-        k_bl_final<1><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
-        if (count > 0) k_bl_apply<float><<<ab, 256, 0, s>>>((const float*)x, (float*)out, count, op, stats);
+        nw_launch(k_bl_partial<float, 0>, nb, BL_THREADS, 0, s, (const float*)x, b0, b1, stats, part);
+        nw_launch(k_bl_final<0>, 1, BL_THREADS, 0, s, part, nb, n, stats);
+        nw_launch(k_bl_partial<float, 1>, nb, BL_THREADS, 0, s, (const float*)x, b0, b1, stats, part);
+        nw_launch(k_bl_final<1>, 1, BL_THREADS, 0, s, part, nb, n, stats);
+        if (count > 0) nw_launch(k_bl_apply<float>, ab, 256, 0, s, (const float*)x, (float*)out, count, op, stats);
     } else {
-        k_bl_partial<double, 0><<<nb, BL_THREADS, 0, s>>>((const double*)x, b0, b1, stats, part);
-        k_bl_final<0><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
-        k_bl_partial<double, 1><<<nb, BL_THREADS, 0, s>>>((const double*)x, b0, b1, stats, part);
-        k_bl_final<1><<<1, BL_THREADS, 0, s>>>(part, nb, n, stats);
-        if (count > 0) k_bl_apply<double><<<ab, 256, 0, s>>>((const double*)x, (double*)out, count, op, stats);
+        nw_launch(k_bl_partial<double, 0>, nb, BL_THREADS, 0, s, (const double*)x, b0, b1, stats, part);
+        nw_launch(k_bl_final<0>, 1, BL_THREADS, 0, s, part, nb, n, stats);
+        nw_launch(k_bl_partial<double, 1>, nb, BL_THREADS, 0, s, (const double*)x, b0, b1, stats, part);
+        nw_launch(k_bl_final<1>, 1, BL_THREADS, 0, s, part, nb, n, stats);
+        if (count > 0) nw_launch(k_bl_apply<double>, ab, 256, 0, s, (const double*)x, (double*)out, count, op, stats);
     }
     return hipGetLastError();
 }
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(256) void k_gather_elems(const uint32_t* __restrict
 __global__ __launch_bounds__(64) void k_dcheck_selftest(int n) { NW_DCHECK((int)threadIdx.x < n); }
 
 hipError_t launch_dcheck_selftest(hipStream_t s) {
-    k_dcheck_selftest<<<1, 64, 0, s>>>(32);
+    nw_launch(k_dcheck_selftest, 1, 64, 0, s, 32);
     return hipGetLastError();
 }
 
@@ -526,7 +526,7 @@ hipError_t launch_gather(const void* src, void* dst, const int32_t* idx, int cou
     if (elem_bytes % 4) return hipErrorInvalidValue;
     const int64_t words = (int64_t)(elem_bytes / 4);
     const int64_t blocks = std::min<int64_t>(((int64_t)count * words + 255) / 256, int64_t(1) << 16);
-    k_gather_elems<<<(unsigned)blocks, 256, 0, s>>>((const uint32_t*)src, (uint32_t*)dst, idx, count, words);
+    nw_launch(k_gather_elems, (unsigned)blocks, 256, 0, s, (const uint32_t*)src, (uint32_t*)dst, idx, count, words);
     return hipGetLastError();
 }
 
@@ -541,7 +541,7 @@ hipError_t launch_expand_rows(const void* src, void* dst, int64_t nsig, int nu, 
         const int64_t nblk = nsig * nu * tiles;
         if (nblk == 0) return;
         const int64_t grid = std::min<int64_t>(nblk, int64_t(1) << 20);
-        k_expand_rows<V><<<(unsigned)grid, 256, 0, s>>>((const V*)src, (V*)dst, rowv, tiles, nblk, nu, nf, offs, order);
+        nw_launch(k_expand_rows<V>, (unsigned)grid, 256, 0, s, (const V*)src, (V*)dst, rowv, tiles, nblk, nu, nf, offs, order);
     };
     if (row_bytes % 16 == 0) go((V4*)nullptr, 16);
     else if (row_bytes % 8 == 0) go((V2*)nullptr, 8);

@@ -1093,7 +1093,7 @@ hipError_t launch_row_pass(const WDesc& d, int f0, int nf, int n1, const C2<T>* 
     const int gpad = (ngroups + 8 * kRowTileG - 1) / (8 * kRowTileG) * (8 * kRowTileG);
     const int nfr = (nf + kRowTileF - 1) / kRowTileF;
     const int64_t blocks = (int64_t)gpad * nfr * kRowTileF;
-    rows_kernel<T, N2, E, KIND><<<(unsigned)blocks, N2 / E, lds, s>>>(d, f0, nf, n1, rgs, Xt, B, kmax,
+    nw_launch(rows_kernel<T, N2, E, KIND>, (unsigned)blocks, N2 / E, lds, s, d, f0, nf, n1, rgs, Xt, B, kmax,
                                                                        reinterpret_cast<const C2<T>*>(tw));
     return hipGetLastError();
 }
@@ -1113,11 +1113,11 @@ hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, 
         hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
         if (e != hipSuccess) return e;
         if (out_kind == NW_OUT_CWT)
-            cols_kernel<N1, N2, NW_OUT_CWT><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
+            nw_launch(cols_kernel<N1, N2, NW_OUT_CWT>, (unsigned)blocks, CL::THREADS, lds, s, f0, nf, B, out);
         else if (out_kind == NW_OUT_POWER)
-            cols_kernel<N1, N2, NW_OUT_POWER><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
+            nw_launch(cols_kernel<N1, N2, NW_OUT_POWER>, (unsigned)blocks, CL::THREADS, lds, s, f0, nf, B, out);
         else
-            cols_kernel<N1, N2, NW_OUT_ABS><<<(unsigned)blocks, CL::THREADS, lds, s>>>(f0, nf, B, out);
+            nw_launch(cols_kernel<N1, N2, NW_OUT_ABS>, (unsigned)blocks, CL::THREADS, lds, s, f0, nf, B, out);
         return hipGetLastError();
     }
     using CL = Cols<T, N1>;
@@ -1137,11 +1137,11 @@ hipError_t launch_cols(int out_kind, int f0, int nf, const C2<T>* B, void* out, 
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     if (out_kind == NW_OUT_CWT)
-        cols_kernel<T, N1, N2, NW_OUT_CWT><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
+        nw_launch(cols_kernel<T, N1, N2, NW_OUT_CWT>, (unsigned)blocks, kColThreads<T>, lds, s, f0, nf, B, out, tw1, tsplit);
     else if (out_kind == NW_OUT_POWER)
-        cols_kernel<T, N1, N2, NW_OUT_POWER><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
+        nw_launch(cols_kernel<T, N1, N2, NW_OUT_POWER>, (unsigned)blocks, kColThreads<T>, lds, s, f0, nf, B, out, tw1, tsplit);
     else
-        cols_kernel<T, N1, N2, NW_OUT_ABS><<<(unsigned)blocks, kColThreads<T>, lds, s>>>(f0, nf, B, out, tw1, tsplit);
+        nw_launch(cols_kernel<T, N1, N2, NW_OUT_ABS>, (unsigned)blocks, kColThreads<T>, lds, s, f0, nf, B, out, tw1, tsplit);
     return hipGetLastError();
 }
 
@@ -1195,23 +1195,23 @@ hipError_t large_row_support(const WDesc& d, int dtype, void* support, bool scan
     e = hipMemsetAsync(wmax, 0, (size_t)d.nfreq * sizeof(uint64_t), s);            // +0.0
     if (e != hipSuccess) return e;
     if (!scan && support_fast_ok(d, dtype)) {
-        if (dtype == NW_F32) support_fast_kernel<float><<<d.nfreq, kFastThreads, 0, s>>>(d, kmax, wmax);
-        else support_fast_kernel<double><<<d.nfreq, kFastThreads, 0, s>>>(d, kmax, wmax);
+        if (dtype == NW_F32) nw_launch(support_fast_kernel<float>, d.nfreq, kFastThreads, 0, s, d, kmax, wmax);
+        else nw_launch(support_fast_kernel<double>, d.nfreq, kFastThreads, 0, s, d, kmax, wmax);
         return hipGetLastError();
     }
     const int64_t per_block = 256 * kSupBins;
     dim3 grid((unsigned)((d.n + per_block - 1) / per_block), (unsigned)d.nfreq);
     const bool realw = d.kind != NW_TABLE;
     if (dtype == NW_F32) {
-        if (realw) wmax_kernel<float, true><<<grid, 256, 0, s>>>(d, wmax);
-        else wmax_kernel<float, false><<<grid, 256, 0, s>>>(d, wmax);
-        if (realw) kmax_kernel<float, true><<<grid, 256, 0, s>>>(d, kmax, wmax);
-        else kmax_kernel<float, false><<<grid, 256, 0, s>>>(d, kmax, wmax);
+        if (realw) nw_launch(wmax_kernel<float, true>, grid, 256, 0, s, d, wmax);
+        else nw_launch(wmax_kernel<float, false>, grid, 256, 0, s, d, wmax);
+        if (realw) nw_launch(kmax_kernel<float, true>, grid, 256, 0, s, d, kmax, wmax);
+        else nw_launch(kmax_kernel<float, false>, grid, 256, 0, s, d, kmax, wmax);
     } else {
-        if (realw) wmax_kernel<double, true><<<grid, 256, 0, s>>>(d, wmax);
-        else wmax_kernel<double, false><<<grid, 256, 0, s>>>(d, wmax);
-        if (realw) kmax_kernel<double, true><<<grid, 256, 0, s>>>(d, kmax, wmax);
-        else kmax_kernel<double, false><<<grid, 256, 0, s>>>(d, kmax, wmax);
+        if (realw) nw_launch(wmax_kernel<double, true>, grid, 256, 0, s, d, wmax);
+        else nw_launch(wmax_kernel<double, false>, grid, 256, 0, s, d, wmax);
+        if (realw) nw_launch(kmax_kernel<double, true>, grid, 256, 0, s, d, kmax, wmax);
+        else nw_launch(kmax_kernel<double, false>, grid, 256, 0, s, d, kmax, wmax);
     }
     return hipGetLastError();
 }
@@ -1225,7 +1225,7 @@ hipError_t build_large_support(const WDesc& d, int dtype, void* support, hipStre
     hipError_t e = large_row_support(d, dtype, support, force_scan, s);
     if (e != hipSuccess) return e;
     if (dtype == NW_F64) {
-        tsplit_kernel<<<kSplitEntries / 256, 256, 0, s>>>(
+        nw_launch(tsplit_kernel, kSplitEntries / 256, 256, 0, s, 
             reinterpret_cast<C2<double>*>(reinterpret_cast<char*>(support) + tsplit_offset(d.nfreq)), d.n);
     }
     return hipGetLastError();
@@ -1238,10 +1238,10 @@ hipError_t large_transpose(const WDesc& d, int dtype, const void* X, void* scrat
     const Split sp = split_of(d.n, dtype);
     const dim3 grid((unsigned)(sp.n1 / 32), (unsigned)(sp.n2 / 32));
     if (dtype == NW_F32)
-        xt_kernel<float><<<grid, 256, 0, s>>>(d, reinterpret_cast<const cplx<float>*>(X),
+        nw_launch(xt_kernel<float>, grid, 256, 0, s, d, reinterpret_cast<const cplx<float>*>(X),
                                               reinterpret_cast<C2<float>*>(scratch), sp.n1, sp.n2);
     else
-        xt_kernel<double><<<grid, 256, 0, s>>>(d, reinterpret_cast<const cplx<double>*>(X),
+        nw_launch(xt_kernel<double>, grid, 256, 0, s, d, reinterpret_cast<const cplx<double>*>(X),
                                                reinterpret_cast<C2<double>*>(scratch), sp.n1, sp.n2);
     return hipGetLastError();
 }

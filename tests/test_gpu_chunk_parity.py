@@ -39,7 +39,7 @@ def fused_constants():
     """kGroup / kGroup64 / kTileG as the kernel source defines them (the launch geometry)."""
     src = open(os.path.join(ROOT, 'ninwavelets_amd', 'csrc', 'nw_fused.hip')).read()
     g = int(re.search(r'constexpr int kGroup = (\d+);', src).group(1))
-    g64 = int(re.search(r'constexpr int kGroup64 = (\d+);', src).group(1))
+    g64 = int(re.search(r'#define NW_GROUP64 (\d+)', src).group(1))
     tg = int(re.search(r'constexpr int kTileF = \d+, kTileG = (\d+);', src).group(1))
     return g, g64, tg
 
