@@ -302,8 +302,11 @@ def run_leg(args, torch, dist, nw, L, world, rank, dev, backend, cfg_name, dtype
     odt = {('cwt', False): torch.complex64, ('cwt', True): torch.complex128}.get(
         (out_kind, f64), torch.float64 if f64 else torch.float32)
     bufs = [torch.empty((C, F, n), dtype=odt, device=dev) for _ in range(1 if C >= S else 2)]
+    # HIP events on the plan's own (dedicated) stream: each stage's stop event rides on its
+    # kernel dispatch and its start is the previous stage's stop (NW_TIMING_CHAIN), so the
+    # timed steps carry no event marker packets
     plan = nw.Plan(n, F, dtype, device=dev.index, max_batch=C,
-                   engine=None if args.engine == 'auto' else args.engine, timing=True)
+                   engine=None if args.engine == 'auto' else args.engine, timing=True, timing_chain=True)
     grid = L.trans_grid(n / 1000., 1000., False)
     params = {'morse': [17.5, 3.0], 'morlet': [7.0, 0.0], 'shannon': []}[kind]
     plan.set_wavelet(kind, params, freqs, grid)

@@ -63,6 +63,12 @@ extern "C" {
                                   of two >= 1024 with 2n-1 <= 16384 fp32 / 8192 fp64: the
                                   chirp-z form, nw_chirp.hip)                                  */
 #define NW_TIMING        0x100u/* record HIP events around every stage (nw_plan_stats)            */
+#define NW_TIMING_CHAIN  0x800u/* with NW_TIMING: the plan's stream carries nothing but this plan's
+                                  executes between two nw_plan_sync / nw_plan_stats calls (a
+                                  dedicated benchmark stream), so each stage -- the first of an
+                                  execute too -- starts at the previous stage's end event and no
+                                  event marker enters the stream (the stop events ride on the
+                                  kernel dispatches themselves)                                 */
 #define NW_NO_CHIRP      0x400u/* auto engine: keep the rocFFT engine for lengths the chirp-z fused
                                   form would take (non-power-of-two n, 2n-1 <= 16384 fp32 /
                                   8192 fp64, and n < 1024; up to n < 16384 / 8192 when every

@@ -33,6 +33,7 @@ NW_INTERPOLATE = 0x1
 NW_ENGINE_ROCFFT = 0x10
 NW_ENGINE_FUSED = 0x20
 NW_TIMING = 0x100
+NW_TIMING_CHAIN = 0x800
 NW_NO_DEDUP = 0x200
 NW_NO_CHIRP = 0x400
 NW_OUT_CWT, NW_OUT_ABS, NW_OUT_POWER = 0, 1, 2

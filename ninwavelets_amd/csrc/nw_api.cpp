@@ -299,7 +299,7 @@ int staged(nw_plan* p, int stage, F&& fn, bool chain = false) {
             stage == ST_FUSED || stage == ST_ROWS ? kernel_name(p->stats.kernel) : "");
     if (!(p->flags & NW_TIMING)) return fn();
     Pending pe{stage, nullptr, nullptr};
-    if (chain && !p->pending.empty()) {
+    if ((chain || (p->flags & NW_TIMING_CHAIN)) && !p->pending.empty()) {
         pe.a = p->pending.back().b;
         pe.own_a = false;
     } else {
@@ -325,7 +325,7 @@ int staged_k(nw_plan* p, int stage, F&& fn, bool chain = false) {
     nw_logf(2, "plan %p: launch %s%s%s", (void*)p, kStageName[stage], stage == ST_FUSED || stage == ST_ROWS ? ": " : "",
             stage == ST_FUSED || stage == ST_ROWS ? kernel_name(p->stats.kernel) : "");
     Pending pe{stage, nullptr, nullptr};
-    const bool chained = chain && !p->pending.empty();
+    const bool chained = (chain || (p->flags & NW_TIMING_CHAIN)) && !p->pending.empty();
     if (chained) {
         pe.a = p->pending.back().b;
         pe.own_a = false;

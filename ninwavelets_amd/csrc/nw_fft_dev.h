@@ -14,7 +14,10 @@
 // unpaired last pass: lane-pair transposes (DPP) regroup outputs of <= 8 B into 16-B stores
 // (pairs of 8-B outputs: n = 4096 cwt 0.413 -> 0.403 ms); 4-B outputs stay single stores
 // (quads: 0.337 -> 0.360 ms at n = 4096 power, pairs: C3 1.253 -> 1.277 ms)
-constexpr int kPackMax = 2;
+#ifndef NW_PACK_MAX   // diagnostic A/B (-DNW_PACK_MAX=4: quad-packed 4-B outputs)
+#define NW_PACK_MAX 2
+#endif
+constexpr int kPackMax = NW_PACK_MAX;
 // smallest pass-0 variant: a W row's support is rounded up to it (1 and 2 add code without a
 // measurable gain)
 constexpr int kPruneMin = 4;

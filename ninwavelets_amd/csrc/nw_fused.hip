@@ -410,7 +410,11 @@ __global__ __launch_bounds__(N / E, OUT == kOutPSum ? 3 : 4) void nw_fused_pair_
     // bins by scalar loads
     // (cwt only: n = 4096 cwt 1.585 -> 1.567 ms per 256-signal launch; |y|^2 slower, C3 1.180 ->
     // 1.210, n = 1024 power equal)
+#ifdef NW_PAIR_XD_ALL   // diagnostic A/B: the LDS-DMA for every output kind
+    constexpr bool XD = kPairXD && OUT != kOutPSum;
+#else
     constexpr bool XD = kPairXD && OUT == NW_OUT_CWT;
+#endif
     const int nzv = nz < kPruneMin ? kPruneMin : nz;
     const int dma_rounds = nzv <= E / 2 ? dma_rounds_for<float>(nzv) : 1 << 30;
     unsigned long long nyq_a = 0, nyq_b = 0;

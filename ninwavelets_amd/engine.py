@@ -239,7 +239,7 @@ class Plan:
 
     def __init__(self, n: int, nfreq: int, dtype='float32', device: int = 0, max_batch: int = 1,
                  interpolate: bool = False, engine: str | None = None, timing: bool = False,
-                 dedup: bool = True):
+                 dedup: bool = True, timing_chain: bool = False):
         self.n, self.nfreq, self.device, self.max_batch = int(n), int(nfreq), int(device), int(max_batch)
         self.dtype = np_dtype(dtype)
         self.interpolate = bool(interpolate)
@@ -252,6 +252,8 @@ class Plan:
             raise ValueError(f'engine must be rocfft, fused or auto, got {engine!r}')
         if timing:
             flags |= L.NW_TIMING
+            if timing_chain:     # a dedicated stream: stage events chained across executes
+                flags |= L.NW_TIMING_CHAIN
         if not dedup:            # compute every scale row even when wavelet rows repeat
             flags |= L.NW_NO_DEDUP
         self._h = ctypes.c_void_p()
