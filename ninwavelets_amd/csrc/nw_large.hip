@@ -78,6 +78,9 @@ template <typename T> constexpr int kColE = 32;
 #endif
 // rows of at most 16384 on chip, fp64 too (N2 = 8192 with N1 = 2048, 8-column blocks and
 // 128-B runs: C5 fp64 150.0 ms/step; 16384, 16 columns, 256-B runs: 129.9)
+// (fp32 rows of 32768 -- N1 = 512, 64-column workgroups writing 512-B output pieces -- measured
+// in round 6: the row pass at one 1024-thread block per CU +37-43 %, the column pass 0-3 %
+// faster, C5 step +10 %; profiles/r06_c5_rows32k_ab.txt)
 template <typename T> constexpr int kMaxN2 = 16384;
 
 // ---- X (R2C half spectrum) -> Xt[k1][k2], mirrored + masked (spectrum_bin)
