@@ -73,7 +73,10 @@ constexpr int kWKeep32 = 16, kWKeep32Small = 8;
 // fp64 n = 16384: the pass-1 twiddle table (Tab1) left room for 8 W elements in the 256 VGPRs:
 // C4 shape fp64 8.21 -> 8.02 ms per launch (4: 8.10; 12 / 16 spill 28 / 52 B;
 // profiles/r05_f64_wkeep_ab.txt)
-constexpr int kWKeep64 = 8;
+#ifndef NW_WKEEP64   // diagnostic A/B
+#define NW_WKEEP64 8
+#endif
+constexpr int kWKeep64 = NW_WKEEP64;
 // the pair kernel (E = 16): W elements kept in registers for the block (nw_fused_pair_kernel)
 constexpr int kPairWKeep = 12;
 // ... in the |y| and power-partial pair kernels (their sqrt / fp64 accumulators take the registers)
@@ -152,7 +155,10 @@ constexpr int kWpsF32 = 4, kWpsF64 = 2, kWpsPhSum = 3, kWpsPSum32 = 2;
 // "Two waves per SIMD", item 4: at equal priority the younger half loses every arbitration).
 // fp64 C4 shape 7.92-7.99 -> 7.89-7.90 ms per launch; fp32 C4 +-0, C3 (signal pairs) +10 %:
 // fp64 only (tools/ab.sh, profiles/r04_ab_fused.txt)
-template <typename T> constexpr bool kPrioHalf = sizeof(T) == 8;
+#ifndef NW_PRIO64   // diagnostic A/B (-DNW_PRIO64=0)
+#define NW_PRIO64 1
+#endif
+template <typename T> constexpr bool kPrioHalf = sizeof(T) == 8 && NW_PRIO64;
 __device__ __forceinline__ void prio_half(int t, int threads) {
     if (__builtin_amdgcn_readfirstlane(t) >= threads / 2) __builtin_amdgcn_s_setprio(1);
 }
