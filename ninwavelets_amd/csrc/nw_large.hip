@@ -230,7 +230,8 @@ __global__ __launch_bounds__(kFastThreads) void support_fast_kernel(WDesc d, int
             if (!(c <= 1.7976931348623157e308)) bad = true;
             else if (c > v) { v = c; kv = k; }
         }
-        if (__syncthreads_or(bad)) break;
+        bad = __syncthreads_or(bad);            // block-wide: the branch below holds barriers
+        if (bad) break;
         blk_max_arg(v, kv, sv, sk);
         M = v;
         m = kv;
