@@ -474,9 +474,11 @@ def roofline_of(args, cfg_name, st, S, F, n, C, out_kind, dtype, esz, el, L):
 LEGS = {'fp64': ('c4', 'float64'), 'c2': ('c2', 'float32'), 'c3': ('c3', 'float32'), 'c5': ('c5', 'float32'),
         'c5_fp64': ('c5', 'float64')}
 # at least this many timed steps / warmups for a leg whose step is short (C2: one 0.2-0.25 ms
-# launch; 3 steps time < 1 ms and vary +-10 % with the clock ramp), so each leg's timed region
-# runs >= ~10 ms; the headline line keeps exactly --steps / --warmup
-LEG_MIN_STEPS = {'c2': (40, 5)}
+# launch). The clock ramps for tens of ms after an idle gap: 3 steps (< 1 ms) varied +-10 %, and
+# 40 steps after 5 warmups (10 ms) still ran 0.274 ms per step where 400 after 40 ran 0.224 on
+# the same box (profiles/r06_c2_steps_ab.txt), so the leg times ~90 ms of steady state after
+# ~10 ms of warmup; the headline line keeps exactly --steps / --warmup
+LEG_MIN_STEPS = {'c2': (400, 40)}
 
 
 def leg_fields(r, st, ex):

@@ -2,8 +2,11 @@
 
 C2 (Morlet cwt 64 x 16384 x 128 fp32) is one forward R2C launch + one fused launch per step.
 This runs the bench's C2 step loop in three forms on one plan and prints one JSON line:
-  timing:    the bench's plan (NW_TIMING: events around every launch), K steps;
+  timing:    a plan with NW_TIMING (events around every launch), K steps;
+  chain:     the bench's plan (NW_TIMING | NW_TIMING_CHAIN: stop events ride on the dispatches,
+             every stage starts at the previous stage's stop, no marker packets);
   notiming:  the same loop on a plan without events;
+(--reps R repeats the chain / notiming pair R times, alternating, on one box.)
   enqueue:   host time to enqueue K steps without waiting (is the host the bound?).
 Run it under `rocprofv3 --kernel-trace` to get the kernels' own timeline (tools/trace_gaps.py).
     python tools/c2_gap.py [--steps 40] [--warmup 5]
@@ -23,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--steps', type=int, default=40)
     ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--reps', type=int, default=1)
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -37,8 +41,11 @@ def main():
     out = torch.empty((S, F, n), dtype=torch.complex64, device=dev)
     grid = L.trans_grid(n / 1000., 1000., False)
     res = {}
-    for name, timing in (('timing', True), ('notiming', False)):
-        plan = nw.Plan(n, F, 'float32', device=0, max_batch=S, timing=timing)
+    forms = [('timing', True, False)] + [(f'{nm}{i if args.reps > 1 else ""}', t, c)
+                                         for i in range(args.reps)
+                                         for nm, t, c in (('chain', True, True), ('notiming', False, False))]
+    for name, timing, chain in forms:
+        plan = nw.Plan(n, F, 'float32', device=0, max_batch=S, timing=timing, timing_chain=chain)
         plan.set_wavelet('morlet', [7.0, 0.0], freqs, grid)
 
         def step():
