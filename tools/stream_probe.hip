@@ -55,7 +55,9 @@ __global__ __launch_bounds__(1024) void copy_kernel(const f4* __restrict__ src, 
 // resident on one XCD at a time hold ADJACENT column groups (their pieces of one output row
 // form one 8-KiB span); false: consecutive workgroups (on 8 different XCDs) take adjacent
 // groups.  NT: nontemporal stores (the product's), else plain (write-back through L2).
-template <int C, bool RS = true, bool WS = true, bool XCD = false, bool NT = true>
+// ROT: output row order rotated per workgroup, n1 -> (n1 + g * ROT) % N1 (0: the product's order,
+// every workgroup walks the rows from 0 at the same time)
+template <int C, bool RS = true, bool WS = true, bool XCD = false, bool NT = true, int ROT = 0>
 __global__ __launch_bounds__(1024) void cols_kernel(const f4* __restrict__ B, f4* __restrict__ out, int nf) {
     constexpr int LANES = C / 2;             // float4 per piece
     constexpr int ROWS = 1024 / LANES;       // k1 rows per pass over the threads
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(1024) void cols_kernel(const f4* __restrict__ B, f4
         }
 #pragma unroll
         for (int i = 0; i < CH; ++i) {
-            const int n1 = row0 + (c0 + i) * ROWS;     // output row n1: out[f][g*C + n2 + N2*n1]
+            const int n1 = (row0 + (c0 + i) * ROWS + g * ROT) & (N1 - 1);   // output row n1: out[f][g*C + n2 + N2*n1]
             const long wo = WS ? ((long)n1 * N2 + (long)g * C) / 2 + lane : (long)g * (N1 * C / 2) + (long)n1 * LANES + lane;
             if constexpr (NT) __builtin_nontemporal_store(v[i], out + fb + wo);
             else out[fb + wo] = v[i];
@@ -148,6 +150,14 @@ int main(int argc, char** argv) {
          [&] { cols_kernel<32, true, true, true, true><<<nf * (N2 / 32), 1024>>>(B, out, nf); });
     time("cols32 XCD-adjacent groups, plain stores", 2.0 * bytes,
          [&] { cols_kernel<32, true, true, true, false><<<nf * (N2 / 32), 1024>>>(B, out, nf); });
+    time("cols32 rows rotated by 37 per group", 2.0 * bytes,
+         [&] { cols_kernel<32, true, true, false, true, 37><<<nf * (N2 / 32), 1024>>>(B, out, nf); });
+    time("cols32 rows rotated by 128 per group", 2.0 * bytes,
+         [&] { cols_kernel<32, true, true, false, true, 128><<<nf * (N2 / 32), 1024>>>(B, out, nf); });
+    time("cols32 rows rotated by 1 per group", 2.0 * bytes,
+         [&] { cols_kernel<32, true, true, false, true, 1><<<nf * (N2 / 32), 1024>>>(B, out, nf); });
+    time("cols32 rows rotated by 32 per group", 2.0 * bytes,
+         [&] { cols_kernel<32, true, true, false, true, 32><<<nf * (N2 / 32), 1024>>>(B, out, nf); });
     time("rows (contiguous write only)", 1.0 * bytes, [&] { rows_kernel<<<cblocks, 1024>>>(B, n4); });
     CHECK(hipFree(B));
     CHECK(hipFree(out));
