@@ -3,6 +3,8 @@
 # kernel-trace --stats and PMC passes (traffic tied to the engine-source hash) for C4, C3,
 # C5 (fp32, fp64), C2 and the fp64 C4 shape.  Output under $REC (default gpurun_out/rec/); stops at the first
 # failure; tools/collect.sh copies it into profiles/.  CFGS selects configs, SKIP_TESTS=1 the tests.
+# (C2, one 0.2 ms launch per step, runs 400 steps after 40 warmups as its default-line leg does:
+# shorter runs sit inside the clock ramp, profiles/r06_c2_steps_ab.txt)
 set -u
 export PYTHONDONTWRITEBYTECODE=1 TMPDIR=/tmp
 R=${REC:-gpurun_out/rec}; mkdir -p $R
@@ -27,7 +29,7 @@ CFGS=${CFGS:-c4 c2 c3 c5 c5f64 c4f64}
 for c in $CFGS; do
   case $c in
     c4) record c4 "--steps 10 --warmup 3" "--config c4 --steps 2 --warmup 1 --legs none" "nw_fused_kernel" '{"chunk": 512, "n": 16384, "freqs": 256, "out": "cwt", "dtype": "float32"}' || exit $? ;;
-    c2) record c2 "--config c2 --steps 20 --warmup 3" "--config c2 --steps 5 --warmup 1" "nw_fused_kernel" '{"chunk": 64, "n": 16384, "freqs": 128, "out": "cwt", "dtype": "float32"}' || exit $? ;;
+    c2) record c2 "--config c2 --steps 400 --warmup 40" "--config c2 --steps 400 --warmup 40" "nw_fused_kernel" '{"chunk": 64, "n": 16384, "freqs": 128, "out": "cwt", "dtype": "float32"}' || exit $? ;;
     c3) record c3 "--config c3 --steps 5 --warmup 2" "--config c3 --steps 2 --warmup 1" "nw_fused_pair_kernel" '{"chunk": 1024, "n": 4096, "freqs": 256, "out": "power", "dtype": "float32"}' || exit $? ;;
     c5) record c5 "--config c5 --steps 3 --warmup 1" "--config c5 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float32", "scales_per_launch": 64}' || exit $? ;;
     c5f64) record c5f64 "--config c5 --dtype float64 --steps 3 --warmup 1" "--config c5 --dtype float64 --steps 1 --warmup 1" "cols_kernel rows_kernel" '{"chunk": 1, "n": 16777216, "freqs": 512, "out": "cwt", "dtype": "float64", "scales_per_launch": 32}' || exit $? ;;
