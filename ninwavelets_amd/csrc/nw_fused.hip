@@ -139,6 +139,19 @@ constexpr int kTileF = 8, kTileG = 4;
 #endif
 template <typename T> constexpr int kTileFT = sizeof(T) == 8 ? NW_TILE64_F : kTileF;
 template <typename T> constexpr int kTileGT = sizeof(T) == 8 ? NW_TILE64_G : kTileG;
+// fp64 output kernels at n = 16384 (one block per CU): 16-signal blocks in XCD tiles of 8 scales
+// x 2 groups -- the same X + W working set per XCD round as 8 x 4 of 8 signals, half the blocks
+// (C4 shape fp64 7.175 -> 7.12-7.13 and 7.246 -> 7.212 ms per launch on two boxes, -0.5 %;
+// 32 x 1 -0.3 %, 16 signals in 8 x 4 tiles -0.4 %, 16 in 8 x 1 +-0; profiles/r06_f64_g16_ab.txt).
+// Smaller n (two blocks per CU) and the partial-sum kernels keep kGroup64 / kTileGT.
+#ifndef NW_GROUP64_16K
+#define NW_GROUP64_16K 16
+#endif
+#ifndef NW_TILE64_G_16K
+#define NW_TILE64_G_16K 2
+#endif
+template <typename T, int N> constexpr int kGroupOut = sizeof(T) == 8 ? (N == 16384 ? NW_GROUP64_16K : kGroup64) : kGroup;
+template <typename T, int N> constexpr int kTileGOut = sizeof(T) == 8 && N == 16384 ? NW_TILE64_G_16K : kTileGT<T>;
 // ... and at most as many groups as a launch has (in units of 8 XCD slots): C2 (64 signals =
 // 8 groups) with 4-group tiles padded its grid to 4x its real blocks
 __host__ __device__ constexpr int tile_g_of(int64_t nsg, int tg_max) {
@@ -706,10 +719,10 @@ hipError_t launch_n(const WDesc& d, int out_kind, const void* X, const void* wta
     void* tw = nullptr;
     hipError_t e = twiddles_for(N, sizeof(T) == 4 ? NW_F32 : NW_F64, &tw);
     if (e != hipSuccess) return e;
-    const int grp = kPairMode<T, E, REALW> ? kGroup : group_for(sizeof(T) == 8 ? kGroup64 : kGroup, nsig, d.nfreq);
+    const int grp = kPairMode<T, E, REALW> ? kGroup : group_for(kGroupOut<T, N>, nsig, d.nfreq);
     const int64_t nsg = (nsig + grp - 1) / grp;
     constexpr int TF = kTileFT<T>;
-    const int TG = tile_g_of(nsg, kTileGT<T>);
+    const int TG = tile_g_of(nsg, kTileGOut<T, N>);
     const int64_t nsg_pad = (nsg + 8 * TG - 1) / (8 * TG) * (8 * TG);
     const int64_t nfr = (d.nfreq + TF - 1) / TF;
     const int64_t blocks = nsg_pad * nfr * TF;

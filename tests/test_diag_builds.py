@@ -16,7 +16,8 @@ CSRC = os.path.join(ROOT, 'ninwavelets_amd', 'csrc')
 SWITCHES = {
     'nw_fused.hip': ['NW_ABL_NOWLOAD', 'NW_STAMPS', 'NW_ABL_NOSTORE', 'NW_ABL_NOTWIDDLE', 'NW_ABL_NOEXCH',
                      'NW_PAIR_PAD16=0', 'NW_TAIL_EXACT', 'NW_PACK_MAX=4', 'NW_PAIR_XD_ALL', 'NW_F64_FINE=0',
-                     'NW_GROUP64=4', 'NW_TILE64_F=4', 'NW_TILE64_G=8', 'NW_WKEEP64=4', 'NW_PRIO64=0'],
+                     'NW_GROUP64=4', 'NW_TILE64_F=4', 'NW_TILE64_G=8', 'NW_WKEEP64=4', 'NW_PRIO64=0',
+                     'NW_GROUP64_16K=8', 'NW_TILE64_G_16K=4'],
     'nw_large.hip': ['NW_ABL_ROWS_NOW', 'NW_B_PLAIN', 'NW_ABL_COLS_NOFFT', 'NW_ABL_COLS_NOSTORE',
                      'NW_ABL_COLS_NOTW', 'NW_ABL_COLS_STREAM', 'NW_ABL_ROWS_STREAM', 'NW_ABL_NOSTORE', 'NW_ABL_NOTWIDDLE', 'NW_ABL_NOEXCH',
                      'NW_ROWS_NO_REC', 'NW_TAIL_EXACT', 'NW_COLS64_E16'],

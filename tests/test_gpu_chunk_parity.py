@@ -35,13 +35,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 TAIL = 37
 
 
-def fused_constants():
-    """kGroup / kGroup64 / kTileG as the kernel source defines them (the launch geometry)."""
+def fused_constants(f64=False):
+    """Signals per block and XCD-tile groups as the kernel source defines them for the
+    n = 16384 output kernels (kGroup / kTileG; fp64: NW_GROUP64_16K / NW_TILE64_G_16K)."""
     src = open(os.path.join(ROOT, 'ninwavelets_amd', 'csrc', 'nw_fused.hip')).read()
+    if f64:
+        return (int(re.search(r'#define NW_GROUP64_16K (\d+)', src).group(1)),
+                int(re.search(r'#define NW_TILE64_G_16K (\d+)', src).group(1)))
     g = int(re.search(r'constexpr int kGroup = (\d+);', src).group(1))
-    g64 = int(re.search(r'#define NW_GROUP64 (\d+)', src).group(1))
     tg = int(re.search(r'constexpr int kTileF = \d+, kTileG = (\d+);', src).group(1))
-    return g, g64, tg
+    return g, tg
 
 
 def synth(S, n, seed, dtype):
@@ -73,8 +76,8 @@ def test_bench_chunk_every_row(n, dtype, chunk, out_kind, kernel):
     f64 = dtype == 'float64'
     S, freqs = chunk + TAIL, np.arange(1, 257, dtype=np.float64)
     F = len(freqs)
-    grp, grp64, tile_g = fused_constants()
-    group = grp64 if f64 else grp
+    assert n == 16384 or not f64
+    group, tile_g = fused_constants(f64)
     nsg = -(-chunk // group)
     nsg_pad = -(-nsg // (8 * tile_g)) * (8 * tile_g)
     assert nsg_pad // (8 * tile_g) >= 2, 'the chunk must span >= 2 XCD-tile G-rounds'
